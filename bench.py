@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""bench.py -- exact k-th selection on MI355X (BASELINE.json metric).
+
+One step = one exact selection of the k-th smallest of n int32 keys already
+resident in HBM (k = n/2, the median, as in the reference's k = n/2 variants
+kth-problem-seq.c~:24 and TODO-kth-problem-cgm.c~:48).
+
+  N = 1 : BASELINE config 2 -- 2^30 keys on one GPU (kth_select_i32_async).
+  N > 1 : BASELINE config 3 -- 2^30 keys per GPU (weak scaling, 2^33 at N = 8),
+          one process per GPU, RCCL collectives through torch.distributed
+          (kselect.dist.DistSelector); value = all ranks' keys / max-over-ranks time.
+
+Input: counter-based synthetic keys generated on the device (family
+uniform_half = [-2^30, 2^30), the reference's well-defined domain, so the CPU
+baselines are correct runs of the reference).  The answer of every run is
+verified on the device with an exact rank certificate (#<v < k <= #<=v).
+
+Extra fields: "roofline" (streaming kernel k_main: 4 B/key algorithmic bytes /
+its HIP-event-timed duration vs 8 TB/s; traffic from profiles/pmc_traffic.json
+when present) and "cpu_baseline" (rank 0, N = 1: the reference's own seq select
+block, vector.c compiled from /root/reference into oracle/_ref, on a bounded
+sample of the same family).
+"""
+import argparse
+import ctypes
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mpi-k-selection_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+class _IntVector(ctypes.Structure):  # reference vector.h:7-11
+    _fields_ = [("size", ctypes.c_int), ("capacity", ctypes.c_int), ("data", ctypes.POINTER(ctypes.c_int))]
+
+
+def cpu_baseline(keys_np, family):
+    """The reference's seq select block (kth-problem-seq.c:30-35: VecQuickSort + VecGet
+    on one core) timed on this host on a bounded sample of the workload."""
+    import numpy as np
+
+    n = keys_np.size
+    k = n // 2
+    ref = os.path.join(REPO, "oracle", "_ref", "libvector_ref.so")
+    buf = np.array(keys_np, dtype=np.int32, copy=True)
+    if os.path.exists(ref):
+        lib = ctypes.CDLL(ref)
+        lib.VecGet.restype = ctypes.c_int
+        v = _IntVector(n, n, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        t0 = time.perf_counter()
+        lib.VecQuickSort(ctypes.byref(v))
+        ans = lib.VecGet(ctypes.byref(v), ctypes.c_int(k - 1))
+        dt = time.perf_counter() - t0
+        kind = "reference"
+        what = "reference vector.c (oracle/_ref/libvector_ref.so): VecQuickSort + VecGet(k-1)"
+    else:
+        lib = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        lib.ko_seq_ref_inplace.restype = ctypes.c_int32
+        lib.ko_seq_ref_inplace.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]
+        t0 = time.perf_counter()
+        ans = lib.ko_seq_ref_inplace(buf.ctypes.data, n, k)
+        dt = time.perf_counter() - t0
+        kind = "port"
+        what = "oracle restatement ko_seq_ref_inplace (qsort + VecGet)"
+    return {
+        "value": n / dt / 1e9,
+        "unit": "Gkeys/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"seq select block, {what}, on 2^{n.bit_length() - 1} keys of {family}, k=n/2, "
+                  f"{dt:.2f} s; host {cpu_model()} ({os.cpu_count()} cpus visible)",
+        "seconds": dt,
+        "answer": int(ans),
+    }
+
+
+def cpu_baseline_cgm(keys_np, procs, timeout=120):
+    """The reference CGM program (TODO-kth-problem-cgm.c, n/k parameterised) under mpirun."""
+    binary = os.path.join(REPO, "oracle", "_ref", "cgm_param")
+    mpirun = "/opt/conda/bin/mpirun"
+    if not (os.path.exists(binary) and os.path.exists(mpirun)):
+        return None
+    n = keys_np.size
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        keys_np.astype("<i4").tofile(f)
+        path = f.name
+    try:
+        env = dict(os.environ, KO_N=str(n), KO_K=str(n // 2), KO_TIME="1", KO_INPUT=path)
+        p = subprocess.run([mpirun, "-n", str(procs), binary], env=env, capture_output=True, text=True,
+                           timeout=timeout)
+        import re
+
+        m = re.search(r"kth element[= ]\s*(-?\d+)\s*\n\s*time:\s*([0-9.]+)", p.stdout)
+        if not m:
+            return {"error": (p.stdout + p.stderr)[-300:]}
+        t = float(m.group(2))
+        return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": procs, "kind": "reference",
+                "sample": f"mpirun -n {procs} CGM (oracle/_ref/cgm_param) on 2^{n.bit_length() - 1} keys, k=n/2, "
+                          f"MPI_Wtime {t:.3f} s (TODO-kth-problem-cgm.c:76,279)",
+                "answer": int(m.group(1))}
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout {timeout}s"}
+    finally:
+        os.unlink(path)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2n", type=int, default=30, help="keys per GPU = 2^log2n")
+    ap.add_argument("--family", default="uniform_half")
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
+    ap.add_argument("--k", type=int, default=0, help="global 1-based rank (default n_total/2)")
+    ap.add_argument("--cpu-log2n", type=int, default=25)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch
+    import torch.distributed as dist
+
+    import kselect
+    from kselect.dist import DistSelector, HipBackend
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    sel = kselect.Selector(local_rank)
+    sel.set_stream(torch.cuda.current_stream(dev))
+    n_local = 1 << args.log2n
+    n_total = n_local * world
+    k = args.k or n_total // 2
+    family = kselect.FAMILIES[args.family]
+    keys = torch.empty(n_local, dtype=torch.int32, device=dev)
+    sel.fill(keys, n_local, family, args.seed, offset=rank * n_local, n_total=n_total)
+    out = torch.zeros(args.warmup + args.steps, dtype=torch.int32, device=dev)
+
+    if world == 1:
+        sel.reserve(n_local)
+
+        def step(i):
+            sel.select_async(keys, n_local, k, out[i:i + 1])
+    else:
+        ds = DistSelector(HipBackend(local_rank, sel))
+
+        def step(i):
+            out[i:i + 1].copy_(ds.select(keys, n_local, n_total, k))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier()
+    sel.enable_timing(True)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    n_sel, main_ms, total_ms = sel.take_timing()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # exact rank certificate of every answer (device-side integer counts)
+    answers = out.cpu().tolist()
+    v = answers[args.warmup]
+    cnt = torch.stack([(keys < v).sum(), (keys <= v).sum()]).to(torch.int64)
+    if world > 1:
+        dist.all_reduce(cnt)
+    lt, le = (int(x) for x in cnt.tolist())
+    verified = (lt < k <= le) and all(a == v for a in answers)
+    stats = sel.stats() if world == 1 else None
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = n_total / (elapsed / args.steps) / 1e9
+    avg_main_ms = main_ms / max(1, n_sel)
+    achieved = 4.0 * n_local / (avg_main_ms * 1e-3) / 1e9 if avg_main_ms > 0 else None
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("log2n") == args.log2n and tj.get("family") == args.family:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    res = {
+        "metric": "Gkeys/s exact k-th select, 2^30 int32 (1 GPU) / 2^33 (8 GPU); % HBM roofline",
+        "value": value,
+        "unit": "Gkeys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (device counter-based generator, splitmix64)",
+        "config": {
+            "workload": f"exact k-th select (median) of 2^{args.log2n} int32 keys per GPU, {args.family}",
+            "n_total": n_total,
+            "k": k,
+            "keys_per_gpu": n_local,
+            "family": args.family,
+            "parallelism": f"shards{world}" if world > 1 else "single",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "kth::k_main (streaming pass)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": 4 * n_local,
+            "avg_launch_ms": avg_main_ms,
+        },
+        "verified": bool(verified),
+        "answer": v,
+        "whole_select_ms_events": total_ms / max(1, n_sel) if world == 1 else None,
+    }
+    if stats:
+        res["path"] = {1: "lds", 2: "radix", 3: "window", 4: "window_fallback"}.get(stats["path"], "?")
+        res["candidates"] = stats["candidates"]
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nc = 1 << args.cpu_log2n
+        tmp = torch.empty(nc, dtype=torch.int32, device=dev)
+        sel.fill(tmp, nc, family, args.seed, offset=0, n_total=nc)
+        keys_np = tmp.cpu().numpy()
+        del tmp
+        try:
+            res["cpu_baseline"] = cpu_baseline(keys_np, args.family)
+            cg = cpu_baseline_cgm(keys_np, min(8, os.cpu_count() or 1))
+            if cg:
+                res["cpu_baseline_cgm"] = cg
+        except Exception as e:  # noqa: BLE001 -- baseline is informational
+            res["cpu_baseline"] = {"error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if verified else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,163 @@
+/*
+ * kth.h -- C-ABI of the MI355X k-th element selection engine (libkth.so).
+ *
+ * Drop-in boundary for laertispappas/MPI-k-selection's selection path.  The
+ * reference has no plugin/FFI layer; its boundary is the C-level contract
+ * (IntVector data, n = data->size, k) -> int value used at
+ *   kth-problem-seq.c:32-33        VecQuickSort(pVec); solution = VecGet(pVec, k-1);
+ *   TODO-kth-problem-cgm.c:76-278  CGM rounds + final gather/sort/VecGet on rank 0
+ * Every entry point below replaces one of those call sites (cited per function).
+ *
+ * Conventions (all functions):
+ *   - k is 1-based, 1 <= k <= n (as in the reference's VecGet(k-1) call sites).
+ *   - Order is signed int32 order (float32: IEEE total order, see rows_f32).
+ *   - The input is NOT modified (the reference sorts in place; both of its
+ *     drivers discard the data afterwards, kth-problem-seq.c:36,
+ *     TODO-kth-problem-cgm.c:283-284, so not mutating is strictly compatible).
+ *   - Return value is 0 (KTH_OK) or a negative KTH_E* code; the answer goes to
+ *     *out, never in-band (the in-band VecGet sentinels live in vector.h's
+ *     VecKthSelect only).
+ *   - Streams are passed as `void *` holding a hipStream_t (NULL = the ctx's own
+ *     stream).  No C++ or framework types cross this boundary.
+ *   - A kth_ctx is not thread-safe: one ctx per host thread or device.
+ *   - The product path has no CPU fallback: without a usable GPU every compute
+ *     entry point returns KTH_ENODEV.
+ */
+#ifndef KTH_H
+#define KTH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KTH_OK 0
+#define KTH_EINVAL (-1)   /* bad n / k / pointer / shape                */
+#define KTH_ENOMEM (-2)   /* device or pinned-host allocation failed    */
+#define KTH_EHIP (-3)     /* HIP runtime or kernel launch error         */
+#define KTH_ENODEV (-4)   /* no HIP device                              */
+#define KTH_EINTERNAL (-5) /* device-side consistency check failed      */
+
+#define KTH_VERSION 1
+
+/* Selection paths (kth_stats.path). */
+#define KTH_PATH_LDS 1      /* n small: one workgroup, keys resident in LDS            */
+#define KTH_PATH_RADIX 2    /* multi-pass radix select over the input                  */
+#define KTH_PATH_WINDOW 3   /* sample window + one streaming pass + candidate radix    */
+#define KTH_PATH_WINDOW_FALLBACK 4 /* window missed -> radix passes over the input     */
+
+typedef struct kth_ctx kth_ctx;
+
+typedef struct kth_stats {
+    int32_t path;          /* KTH_PATH_*                                      */
+    int32_t mode;          /* internal final mode (debug)                     */
+    uint32_t lo_key, hi_key; /* sample window in order-preserving key space   */
+    uint64_t n, k;
+    uint64_t cnt_lt;       /* keys below the window                           */
+    uint64_t cnt_eq_lo, cnt_eq_hi;
+    uint64_t candidates;   /* keys strictly inside the window                 */
+    uint64_t capacity;     /* candidate buffer capacity                       */
+    int32_t answer;
+    int32_t error;         /* device-side error word (0 = none)               */
+} kth_stats;
+
+const char *kth_strerror(int code);
+int kth_version(void);
+int kth_device_count(void);
+
+/* --- one-shot entry point -------------------------------------------------
+ * Replaces kth-problem-seq.c:32-33 and TODO-kth-problem-cgm.c:76-278.
+ * keys may be host or device memory (detected with hipPointerGetAttributes).
+ * Synchronous; uses a lazily created per-thread ctx on device 0. */
+int kth_select_i32(const int32_t *keys, int64_t n, int64_t k, int32_t *out);
+
+/* --- context API (scratch reuse, streams) ---------------------------------- */
+int kth_ctx_create(int device, kth_ctx **ctx);
+int kth_ctx_destroy(kth_ctx *ctx);
+int kth_ctx_set_stream(kth_ctx *ctx, void *hip_stream);
+int kth_ctx_sync(kth_ctx *ctx);
+/* Pre-size scratch for inputs of up to n keys (optional; grows on demand). */
+int kth_ctx_reserve(kth_ctx *ctx, int64_t n);
+
+/* Synchronous select through a ctx; keys host or device.  Same contract as
+ * kth_select_i32. */
+int kth_select_i32_ctx(kth_ctx *ctx, const int32_t *keys, int64_t n, int64_t k, int32_t *out);
+
+/* Asynchronous select: d_keys and d_out are device memory; the work is
+ * enqueued on the ctx stream and *d_out is written on the device.  No host
+ * synchronisation and no allocation once the ctx is reserved for n
+ * (graph-capturable). */
+int kth_select_i32_async(kth_ctx *ctx, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out);
+
+/* Stats of the last select on this ctx (synchronises the ctx stream). */
+int kth_ctx_last_stats(kth_ctx *ctx, kth_stats *st);
+
+/* --- timing (bench) ----------------------------------------------------------
+ * When enabled, every select records HIP events on the ctx stream around the
+ * streaming pass (the dominant kernel) and around the whole select. */
+int kth_ctx_enable_timing(kth_ctx *ctx, int on);
+/* Synchronises; returns sums over the selects since the last call and resets:
+ * *n_selects, *main_ms (sum of dominant-kernel durations), *total_ms. */
+int kth_ctx_take_timing(kth_ctx *ctx, int64_t *n_selects, double *main_ms, double *total_ms);
+
+/* --- batched rows (BASELINE config 5; no reference counterpart) -------------
+ * out[r] = k-th smallest of row r of a rows x cols row-major matrix; one
+ * workgroup per row, row resident in LDS.  1 <= cols <= KTH_ROWS_MAX_COLS.
+ * float32 order: IEEE total order with -0.0 < +0.0 and every NaN last
+ * (a NaN answer is returned as the canonical quiet NaN 0x7FC00000). */
+#define KTH_ROWS_MAX_COLS 16384
+int kth_select_rows_i32(kth_ctx *ctx, const int32_t *d_keys, int64_t rows, int32_t cols, int32_t k,
+                        int32_t *d_out);
+int kth_select_rows_f32(kth_ctx *ctx, const float *d_keys, int64_t rows, int32_t cols, int32_t k,
+                        float *d_out);
+
+/* --- synthetic inputs (bench / tests) --------------------------------------
+ * Fills d_out[0..n) with the keys of global indices offset..offset+n of an
+ * n_total-key input of family `dist` (oracle/kth_oracle.h enum ko_dist;
+ * bit-identical to the CPU generator). */
+int kth_fill_synthetic(kth_ctx *ctx, int32_t *d_out, int64_t n, int64_t offset, int64_t n_total,
+                       int dist, uint64_t seed, int32_t param);
+
+/* --- sharded selection, one process per GPU (TODO-kth-problem-cgm.c:76-278) --
+ * The CGM rounds (local median :125-131, Gather :135-136, weighted median
+ * :139-165, Bcast :168, 3-way count :171-185, Allreduce :190, discard
+ * :194-225, final Gatherv + sort :242-278) become:
+ *   every rank samples its shard -> the samples are all-gathered -> every rank
+ *   derives the same window -> one streaming pass per shard (counts + local
+ *   candidates) -> per-rank histograms are all-reduced (uint64 SUM) after each
+ *   step -> every rank picks the same digit from the same reduced histogram.
+ * The host owns the collectives (RCCL through torch.distributed in
+ * kselect/dist.py, or MPI/RCCL from C); these entry points only enqueue the
+ * per-rank device work on the ctx stream and never synchronise the host.
+ *
+ * d_slots: caller-owned device memory of 3 * KTH_STATS_WORDS uint64 words,
+ * bound by kth_dist_begin for one selection.  kth_dist_scan and
+ * kth_dist_level return the index (0..2) of the slot the caller must
+ * all-reduce (SUM) in place across ranks before the next call; every rank
+ * must make the same sequence of calls.
+ *   kth_dist_begin   bind slots, zero them, set (n_total, k)
+ *   kth_dist_sample  local sample of s_local keys of the shard -> d_sample
+ *                    (order-preserving uint32 keys); caller all-gathers
+ *   kth_dist_window  window from the gathered sample of s_total keys
+ *   kth_dist_scan    streaming pass over the shard            -> slot
+ *   kth_dist_level   level = 0 .. KTH_DIST_LEVELS-1           -> slot
+ *   kth_dist_result  writes the k-th smallest of the union of all shards to
+ *                    *d_out (device) */
+#define KTH_STATS_WORDS (8 + 2 * 2048)
+#define KTH_DIST_LEVELS 3
+int kth_dist_begin(kth_ctx *ctx, uint64_t *d_slots, int64_t n_total, int64_t k);
+int kth_dist_sample(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, uint32_t *d_sample,
+                    int64_t s_local);
+int kth_dist_window(kth_ctx *ctx, const uint32_t *d_sample, int64_t s_total);
+int kth_dist_scan(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local);
+int kth_dist_level(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, int level);
+int kth_dist_result(kth_ctx *ctx, int32_t *d_out);
+/* Default sample size per rank for a shard of n_local keys. */
+int64_t kth_dist_sample_size(int64_t n_local);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KTH_H */

@@ -1,0 +1,658 @@
+// kth_api.hip -- extern "C" boundary of libkth.so (include/kth.h).
+//
+// Host-side orchestration of the kernels in kth_kernels.hip: context and
+// scratch management, path choice, the per-path launch sequences, timing
+// events, and the per-rank steps of the sharded protocol.  No host
+// synchronisation inside a select except in the synchronous wrappers, no
+// allocation once a ctx is reserved, no CPU fallback: without a device every
+// compute entry point returns KTH_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kth.h"
+#include "kth_kernels.hip"
+
+using kth::SelState;
+using kth::StepArgs;
+using kth::u64;
+
+namespace {
+
+constexpr int64_t SMALL_N = 16384;           // LDS path
+constexpr int64_t RADIX_MAX_N = 1ll << 22;   // radix path up to here, window path above
+constexpr int64_t SAMPLE_MAX = 1ll << 20;    // sample keys (single GPU / total over ranks)
+constexpr double WINDOW_Z = 6.0;             // window half-width in sample standard deviations
+constexpr int LEVEL_GRID_MAX = 1024;
+constexpr int GATHER_CHUNKS_PER_WAVE = 16;
+constexpr size_t ISLOT_WORDS = 3 * (size_t)kth::STATS_WORDS + 2;  // 3 slots + cand_count + pad
+constexpr int MAX_EVENTS = 4 * 2048;
+
+#define HIP_TRY(x)                                                                                    \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            if (getenv("KTH_DEBUG")) fprintf(stderr, "kth: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return KTH_EHIP;                                                                          \
+        }                                                                                             \
+    } while (0)
+
+#define KTH_TRY(x)              \
+    do {                        \
+        int r_ = (x);           \
+        if (r_ != KTH_OK) return r_; \
+    } while (0)
+
+}  // namespace
+
+struct kth_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cu = 256;
+    SelState *st = nullptr;   // 2 states (ping-pong)
+    u64 *islots = nullptr;    // ISLOT_WORDS
+    uint32_t *sample = nullptr;
+    u64 sample_cap = 0;
+    uint32_t *cand = nullptr;
+    u64 cand_cap = 0;
+    int32_t *staging = nullptr;
+    u64 staging_cap = 0;
+    int32_t *d_status = nullptr;  // [answer, error]
+    int32_t *h_status = nullptr;  // pinned
+    SelState *h_state = nullptr;  // pinned
+    int last_state = -1;
+    // timing: event pairs around the streaming pass and around whole selects
+    bool timing = false;
+    std::vector<hipEvent_t> ev_main, ev_total;
+    int main_used = 0, total_used = 0;
+    bool dirty = false;  // a launch sequence was cut short: re-zero the slots
+    // sharded protocol
+    u64 *uslots = nullptr;
+    int64_t dist_n = 0, dist_k = 0, dist_cap = 0;
+    int dist_level_next = 0;
+};
+
+namespace {
+
+u64 *islot(kth_ctx *c, int i) { return c->islots + (size_t)i * kth::STATS_WORDS; }
+u64 *cand_count(kth_ctx *c) { return c->islots + 3 * (size_t)kth::STATS_WORDS; }
+
+int set_device(kth_ctx *c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return KTH_OK;
+}
+
+int grow(void **p, u64 *cap, u64 want_bytes) {
+    if (*cap >= want_bytes) return KTH_OK;
+    (void)hipDeviceSynchronize();  // in-flight work may still use the old buffer
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, want_bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return KTH_ENOMEM;
+    }
+    *cap = want_bytes;
+    return KTH_OK;
+}
+
+u64 cand_capacity(int64_t n) { return std::max<u64>(1ull << 20, (u64)n / 32); }
+
+int64_t sample_size(int64_t n) {
+    int64_t s = (n / 64) & ~int64_t(63);
+    return std::min<int64_t>(SAMPLE_MAX, std::max<int64_t>(s, 64));
+}
+
+int reserve_cand(kth_ctx *c, int64_t n) {
+    u64 bytes = cand_capacity(n) * 4;
+    return grow(reinterpret_cast<void **>(&c->cand), &c->cand_cap, bytes);
+}
+
+// Window ranks in a sample of s keys for rank k of n: +-Z sample sigmas.
+void window_ranks(int64_t n, int64_t k, int64_t s, u64 *r_lo, u64 *r_hi) {
+    const double p = (double)k / (double)n;
+    const double r = p * (double)s;
+    const double sig = std::sqrt(std::max(1.0, (double)s * p * (1.0 - p)));
+    const double lo = std::floor(r - WINDOW_Z * sig - 2.0), hi = std::ceil(r + WINDOW_Z * sig + 2.0);
+    *r_lo = lo < 1.0 ? 0 : (u64)lo;                       // 0 = no lower bound
+    *r_hi = hi > (double)s ? (u64)s + 1 : (u64)std::max(1.0, hi);  // s+1 = no upper bound
+}
+
+StepArgs step(kth_ctx *c, int adv, int st_in, int st_out, const u64 *in, u64 *acc, u64 *zero) {
+    StepArgs a;
+    memset(&a, 0, sizeof a);
+    a.st_in = st_in >= 0 ? c->st + st_in : nullptr;
+    a.st_out = c->st + st_out;
+    a.stats_in = in;
+    a.stats_acc = acc;
+    a.stats_zero = zero;
+    a.adv = adv;
+    a.cand = c->cand;
+    a.cand_count = cand_count(c);
+    a.cap = c->cand_cap / 4;
+    return a;
+}
+
+// Record one event of a (start, end) pair; pairs are never split because the
+// pool sizes are even and start/end are always recorded together.
+void ev_mark(kth_ctx *c, std::vector<hipEvent_t> &pool, int &used) {
+    if (!c->timing || used >= (int)pool.size()) return;
+    (void)hipEventRecord(pool[used++], c->stream);
+}
+void ev_main(kth_ctx *c) { ev_mark(c, c->ev_main, c->main_used); }
+void ev_total(kth_ctx *c) { ev_mark(c, c->ev_total, c->total_used); }
+
+int launch_check() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        if (getenv("KTH_DEBUG")) fprintf(stderr, "kth: launch failed: %s\n", hipGetErrorString(e));
+        return KTH_EHIP;
+    }
+    return KTH_OK;
+}
+
+int level_grid(u64 count) {
+    u64 g = (count + kth::LEVEL_MIN_PER_WG - 1) / kth::LEVEL_MIN_PER_WG;
+    return (int)std::max<u64>(1, std::min<u64>(LEVEL_GRID_MAX, g));
+}
+
+// ---------------------------------------------------------------- paths
+int run_small(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+    c->last_state = 1;
+    ev_main(c);
+    kth::k_small<<<1, kth::SMALL_BLOCK, (size_t)n * 4, c->stream>>>(keys, (u64)n, (u64)k, d_out, d_status,
+                                                                    c->st + 1);
+    ev_main(c);
+    return launch_check();
+}
+
+int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+    const int g = level_grid((u64)n);
+    StepArgs a = step(c, kth::ADV_INIT_FULL, -1, 0, nullptr, islot(c, 1), islot(c, 2));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    a.init_n = (u64)n;
+    a.init_k = (u64)k;
+    ev_main(c);  // the first radix pass is the dominant kernel here
+    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    ev_main(c);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), nullptr, nullptr);
+    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
+    c->last_state = 1;
+    return launch_check();
+}
+
+// The main pass + candidate levels + result, shared by the single-GPU window
+// path.  Expects the window state in st[0] and the last sample digit's
+// histogram in islot(0).
+int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+    const int64_t s = sample_size(n);
+    const u64 nchunks = (u64)s / kth::SAMPLE_CHUNK;
+    const u64 stride = (u64)n / nchunks;
+    u64 r_lo, r_hi;
+    window_ranks(n, k, s, &r_lo, &r_hi);
+    KTH_TRY(grow(reinterpret_cast<void **>(&c->sample), &c->sample_cap, (u64)s * 4));
+    KTH_TRY(reserve_cand(c, n));
+
+    // sample + first digit of the sample
+    StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
+    a.init_n = (u64)n;
+    a.init_k = (u64)k;
+    a.init_s = (u64)s;
+    a.r_lo = r_lo;
+    a.r_hi = r_hi;
+    const u64 waves = (nchunks + GATHER_CHUNKS_PER_WAVE - 1) / GATHER_CHUNKS_PER_WAVE;
+    const int gg = (int)std::max<u64>(1, (waves + (kth::BLK / kth::WAVE) - 1) / (kth::BLK / kth::WAVE));
+    kth::k_gather<true><<<gg, kth::BLK, 0, c->stream>>>(a, keys, stride, c->sample, (u64)s);
+    // digits 2, 3 of the sample ranks
+    const int gs = level_grid((u64)s);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
+    a.sample = c->sample;
+    a.sample_count = (u64)s;
+    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
+    a.sample = c->sample;
+    a.sample_count = (u64)s;
+    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    // the streaming pass
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), islot(c, 1), islot(c, 2));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    ev_main(c);
+    kth::k_main<<<c->num_cu * 8, kth::BLK, 0, c->stream>>>(a, c->cand);
+    ev_main(c);
+    // decide + candidate (or fallback) levels
+    const int gl = LEVEL_GRID_MAX;
+    a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), islot(c, 2), islot(c, 0));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 2), islot(c, 0), islot(c, 1));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 1, 0, islot(c, 0), islot(c, 1), islot(c, 2));
+    a.keys = keys;
+    a.n_local = (u64)n;
+    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), nullptr, nullptr);
+    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
+    c->last_state = 1;
+    return launch_check();
+}
+
+int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+    if (!c || !d_keys || (!d_out && !d_status) || n < 1 || k < 1 || k > n) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    if (c->dirty) {
+        HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
+        c->dirty = false;
+    }
+    ev_total(c);
+    int rc;
+    if (n <= SMALL_N)
+        rc = run_small(c, d_keys, n, k, d_out, d_status);
+    else if (n <= RADIX_MAX_N)
+        rc = run_radix(c, d_keys, n, k, d_out, d_status);
+    else
+        rc = run_window(c, d_keys, n, k, d_out, d_status);
+    ev_total(c);
+    if (rc != KTH_OK) c->dirty = true;
+    return rc;
+}
+
+bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t at;
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+thread_local kth_ctx *tl_ctx = nullptr;
+
+}  // namespace
+
+// ====================================================================== API
+extern "C" {
+
+const char *kth_strerror(int code) {
+    switch (code) {
+    case KTH_OK: return "ok";
+    case KTH_EINVAL: return "invalid argument";
+    case KTH_ENOMEM: return "out of memory";
+    case KTH_EHIP: return "HIP runtime error";
+    case KTH_ENODEV: return "no HIP device";
+    case KTH_EINTERNAL: return "device-side consistency check failed";
+    default: return "unknown error";
+    }
+}
+
+int kth_version(void) { return KTH_VERSION; }
+
+int kth_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int kth_ctx_create(int device, kth_ctx **out) {
+    if (!out) return KTH_EINVAL;
+    *out = nullptr;
+    int ndev = kth_device_count();
+    if (ndev <= 0) return KTH_ENODEV;
+    if (device < 0 || device >= ndev) return KTH_EINVAL;
+    kth_ctx *c = new kth_ctx();
+    c->device = device;
+    int rc = KTH_OK;
+    do {
+        if (hipSetDevice(device) != hipSuccess) { rc = KTH_EHIP; break; }
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->num_cu = prop.multiProcessorCount;
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
+        c->own_stream = true;
+        if (hipMalloc(reinterpret_cast<void **>(&c->st), 2 * sizeof(SelState)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&c->islots), ISLOT_WORDS * sizeof(u64)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&c->d_status), 4 * sizeof(int32_t)) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&c->h_status), 4 * sizeof(int32_t), 0) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&c->h_state), sizeof(SelState), 0) != hipSuccess) {
+            rc = KTH_ENOMEM;
+            break;
+        }
+        if (hipMemset(c->st, 0, 2 * sizeof(SelState)) != hipSuccess ||
+            hipMemset(c->islots, 0, ISLOT_WORDS * sizeof(u64)) != hipSuccess) {
+            rc = KTH_EHIP;
+            break;
+        }
+        // dynamic LDS beyond the 64 KiB default for the LDS / rows kernels
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kth::k_small),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, SMALL_N * 4);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kth::k_rows<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, KTH_ROWS_MAX_COLS * 4);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kth::k_rows<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, KTH_ROWS_MAX_COLS * 4);
+        (void)hipGetLastError();
+    } while (0);
+    if (rc != KTH_OK) {
+        kth_ctx_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return KTH_OK;
+}
+
+int kth_ctx_destroy(kth_ctx *c) {
+    if (!c) return KTH_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t e : c->ev_main) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_total) (void)hipEventDestroy(e);
+    if (c->st) (void)hipFree(c->st);
+    if (c->islots) (void)hipFree(c->islots);
+    if (c->sample) (void)hipFree(c->sample);
+    if (c->cand) (void)hipFree(c->cand);
+    if (c->staging) (void)hipFree(c->staging);
+    if (c->d_status) (void)hipFree(c->d_status);
+    if (c->h_status) (void)hipHostFree(c->h_status);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    if (tl_ctx == c) tl_ctx = nullptr;
+    delete c;
+    return KTH_OK;
+}
+
+int kth_ctx_set_stream(kth_ctx *c, void *s) {
+    if (!c) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    if (c->own_stream && c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+        c->own_stream = false;
+        c->stream = nullptr;
+    }
+    if (s) {
+        c->stream = reinterpret_cast<hipStream_t>(s);
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return KTH_OK;
+}
+
+int kth_ctx_sync(kth_ctx *c) {
+    if (!c) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return KTH_OK;
+}
+
+int kth_ctx_reserve(kth_ctx *c, int64_t n) {
+    if (!c || n < 0) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    if (n > RADIX_MAX_N) {
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->sample), &c->sample_cap, (u64)sample_size(n) * 4));
+        KTH_TRY(reserve_cand(c, n));
+    }
+    return KTH_OK;
+}
+
+int kth_select_i32_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out) {
+    if (!d_out) return KTH_EINVAL;
+    return select_async(c, d_keys, n, k, d_out, nullptr);
+}
+
+int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *out) {
+    if (!c || !keys || !out || n < 1 || k < 1 || k > n) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    const int32_t *dk = keys;
+    if (!is_device_ptr(keys)) {
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->staging), &c->staging_cap, (u64)n * 4));
+        HIP_TRY(hipMemcpyAsync(c->staging, keys, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+        dk = c->staging;
+    }
+    KTH_TRY(select_async(c, dk, n, k, nullptr, c->d_status));
+    HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_status[1] != 0) return KTH_EINTERNAL;
+    *out = c->h_status[0];
+    return KTH_OK;
+}
+
+int kth_select_i32(const int32_t *keys, int64_t n, int64_t k, int32_t *out) {
+    if (!keys || !out || n < 1 || k < 1 || k > n) return KTH_EINVAL;
+    if (!tl_ctx) {
+        int dev = 0;
+        if (kth_device_count() <= 0) return KTH_ENODEV;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            (void)hipGetLastError();
+            dev = 0;
+        }
+        KTH_TRY(kth_ctx_create(dev, &tl_ctx));
+    }
+    return kth_select_i32_ctx(tl_ctx, keys, n, k, out);
+}
+
+int kth_ctx_last_stats(kth_ctx *c, kth_stats *out) {
+    if (!c || !out) return KTH_EINVAL;
+    if (c->last_state < 0) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    HIP_TRY(hipMemcpyAsync(c->h_state, c->st + c->last_state, sizeof(SelState), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const SelState &s = *c->h_state;
+    memset(out, 0, sizeof *out);
+    out->path = (int32_t)s.path;
+    out->mode = (int32_t)s.mode;
+    out->lo_key = s.lo;
+    out->hi_key = s.hi;
+    out->n = s.n;
+    out->k = s.k;
+    out->cnt_lt = s.cnt[kth::C_LT];
+    out->cnt_eq_lo = s.cnt[kth::C_EQLO];
+    out->cnt_eq_hi = s.cnt[kth::C_EQHI];
+    out->candidates = s.cnt[kth::C_IN];
+    out->capacity = c->cand_cap / 4;
+    out->answer = (int32_t)(s.answer ^ 0x80000000u);
+    out->error = (int32_t)s.error;
+    return KTH_OK;
+}
+
+int kth_ctx_enable_timing(kth_ctx *c, int on) {
+    if (!c) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    if (on && c->ev_main.empty()) {
+        c->ev_main.resize(MAX_EVENTS);
+        c->ev_total.resize(MAX_EVENTS);
+        for (auto &e : c->ev_main) HIP_TRY(hipEventCreate(&e));
+        for (auto &e : c->ev_total) HIP_TRY(hipEventCreate(&e));
+    }
+    c->timing = on != 0;
+    c->main_used = c->total_used = 0;
+    return KTH_OK;
+}
+
+int kth_ctx_take_timing(kth_ctx *c, int64_t *n_sel, double *main_ms, double *total_ms) {
+    if (!c || !n_sel || !main_ms || !total_ms) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    double m = 0, t = 0;
+    int64_t nm = 0;
+    for (int i = 0; i + 1 < c->main_used; i += 2) {
+        float a = 0;
+        HIP_TRY(hipEventElapsedTime(&a, c->ev_main[i], c->ev_main[i + 1]));
+        m += a;
+        nm++;
+    }
+    for (int i = 0; i + 1 < c->total_used; i += 2) {
+        float b = 0;
+        HIP_TRY(hipEventElapsedTime(&b, c->ev_total[i], c->ev_total[i + 1]));
+        t += b;
+    }
+    c->main_used = c->total_used = 0;
+    *n_sel = nm;
+    *main_ms = m;
+    *total_ms = t;
+    return KTH_OK;
+}
+
+int kth_select_rows_i32(kth_ctx *c, const int32_t *d_keys, int64_t rows, int32_t cols, int32_t k, int32_t *d_out) {
+    if (!c || !d_keys || !d_out || rows < 0 || cols < 1 || cols > KTH_ROWS_MAX_COLS || k < 1 || k > cols)
+        return KTH_EINVAL;
+    if (rows == 0) return KTH_OK;
+    KTH_TRY(set_device(c));
+    const int g = (int)std::min<int64_t>(rows, 1 << 20);
+    kth::k_rows<false><<<g, kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
+        reinterpret_cast<const uint32_t *>(d_keys), (u64)rows, (uint32_t)cols, (u64)k,
+        reinterpret_cast<uint32_t *>(d_out));
+    return launch_check();
+}
+
+int kth_select_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t cols, int32_t k, float *d_out) {
+    if (!c || !d_keys || !d_out || rows < 0 || cols < 1 || cols > KTH_ROWS_MAX_COLS || k < 1 || k > cols)
+        return KTH_EINVAL;
+    if (rows == 0) return KTH_OK;
+    KTH_TRY(set_device(c));
+    const int g = (int)std::min<int64_t>(rows, 1 << 20);
+    kth::k_rows<true><<<g, kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
+        reinterpret_cast<const uint32_t *>(d_keys), (u64)rows, (uint32_t)cols, (u64)k,
+        reinterpret_cast<uint32_t *>(d_out));
+    return launch_check();
+}
+
+int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, int64_t n_total, int dist, uint64_t seed,
+                       int32_t param) {
+    if (!c || (!d_out && n > 0) || n < 0 || offset < 0 || dist < 0 || dist > 7) return KTH_EINVAL;
+    if (n == 0) return KTH_OK;
+    KTH_TRY(set_device(c));
+    uint32_t step = 1;
+    if (n_total > 0 && n_total <= (int64_t)0xFFFFFFFFll) {
+        u64 s = (1ull << 32) / (u64)n_total;
+        step = s > 0xFFFFFFFFull ? 0xFFFFFFFFu : (s ? (uint32_t)s : 1u);
+    }
+    const int g = (int)std::min<int64_t>((n + kth::BLK - 1) / kth::BLK, (int64_t)c->num_cu * 16);
+    kth::k_fill<<<g, kth::BLK, 0, c->stream>>>(d_out, (u64)n, (u64)offset, step, dist, seed, param);
+    return launch_check();
+}
+
+// ------------------------------------------------------- sharded protocol
+int64_t kth_dist_sample_size(int64_t n_local) { return sample_size(n_local); }
+
+int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
+    if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    c->uslots = reinterpret_cast<u64 *>(d_slots);
+    c->dist_n = n_total;
+    c->dist_k = k;
+    c->dist_level_next = 0;
+    HIP_TRY(hipMemsetAsync(d_slots, 0, 3 * (size_t)KTH_STATS_WORDS * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
+    c->dirty = false;
+    return KTH_OK;
+}
+
+int kth_dist_sample(kth_ctx *c, const int32_t *d_keys, int64_t n_local, uint32_t *d_sample, int64_t s_local) {
+    if (!c || !d_keys || !d_sample || s_local < 64 || s_local % 64 || n_local < s_local) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    const u64 nchunks = (u64)s_local / kth::SAMPLE_CHUNK;
+    const u64 stride = (u64)n_local / nchunks;
+    StepArgs a;
+    memset(&a, 0, sizeof a);
+    const u64 waves = (nchunks + GATHER_CHUNKS_PER_WAVE - 1) / GATHER_CHUNKS_PER_WAVE;
+    const int gg = (int)std::max<u64>(1, (waves + 3) / 4);
+    kth::k_gather<false><<<gg, kth::BLK, 0, c->stream>>>(a, d_keys, stride, d_sample, (u64)s_local);
+    return launch_check();
+}
+
+int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
+    if (!c || !d_sample || s_total < 1 || !c->uslots) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    u64 r_lo, r_hi;
+    window_ranks(c->dist_n, c->dist_k, s_total, &r_lo, &r_hi);
+    const int gs = level_grid((u64)s_total);
+    StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
+    a.init_n = (u64)c->dist_n;
+    a.init_k = (u64)c->dist_k;
+    a.init_s = (u64)s_total;
+    a.r_lo = r_lo;
+    a.r_hi = r_hi;
+    a.sample = d_sample;
+    a.sample_count = (u64)s_total;
+    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
+    a.sample = d_sample;
+    a.sample_count = (u64)s_total;
+    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
+    a.sample = d_sample;
+    a.sample_count = (u64)s_total;
+    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    return launch_check();
+}
+
+int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
+    if (!c || !d_keys || n_local < 0 || !c->uslots) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    KTH_TRY(reserve_cand(c, std::max<int64_t>(n_local, 1)));
+    StepArgs a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), c->uslots, nullptr);
+    a.keys = d_keys;
+    a.n_local = (u64)n_local;
+    ev_main(c);
+    kth::k_main<<<c->num_cu * 8, kth::BLK, 0, c->stream>>>(a, c->cand);
+    ev_main(c);
+    c->dist_level_next = 0;
+    KTH_TRY(launch_check());
+    return 0;
+}
+
+int kth_dist_level(kth_ctx *c, const int32_t *d_keys, int64_t n_local, int level) {
+    if (!c || !d_keys || n_local < 0 || !c->uslots || level < 0 || level >= KTH_DIST_LEVELS ||
+        level != c->dist_level_next)
+        return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    u64 *U[3] = {c->uslots, c->uslots + KTH_STATS_WORDS, c->uslots + 2 * KTH_STATS_WORDS};
+    const int in = level % 3, acc = (level + 1) % 3, zero = (level + 2) % 3;
+    // states: scan wrote st[1]; level l reads st[(l+1)%2] and writes st[l%2]
+    StepArgs a = step(c, level == 0 ? kth::ADV_DECIDE : kth::ADV_PICK, (level + 1) % 2, level % 2, U[in], U[acc],
+                      level == 0 ? nullptr : U[zero]);
+    a.keys = d_keys;
+    a.n_local = (u64)n_local;
+    kth::k_level<<<LEVEL_GRID_MAX, kth::BLK, 0, c->stream>>>(a);
+    KTH_TRY(launch_check());
+    c->dist_level_next = level + 1;
+    return acc;
+}
+
+int kth_dist_result(kth_ctx *c, int32_t *d_out) {
+    if (!c || !d_out || !c->uslots || c->dist_level_next != KTH_DIST_LEVELS) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    const int in = KTH_DIST_LEVELS % 3;  // slot written by the last level
+    const int st_in = (KTH_DIST_LEVELS - 1) % 2;
+    StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)in * KTH_STATS_WORDS, nullptr, nullptr);
+    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots, ISLOT_WORDS);
+    c->last_state = 1 - st_in;
+    c->dist_level_next = -1;
+    return launch_check();
+}
+
+}  // extern "C"

@@ -1,0 +1,236 @@
+"""kselect -- Python host mirror of the libkth.so C-ABI (include/kth.h).
+
+Mirrors the reference's selection interface (laertispappas/MPI-k-selection):
+
+  * ``IntVec`` wraps the reference's ``IntVector`` (vector.h:7-11) through
+    the ABI twin in libkth.so; ``IntVec.kth_select(k)`` is the drop-in for the
+    select block ``VecQuickSort(pVec); VecGet(pVec, k - 1)``
+    (kth-problem-seq.c:32-33), keeping the VecGet sentinels (-1 NULL, -2 out of
+    range, vector.c:209-218).
+  * ``kth_select(keys, k)`` / ``Selector`` -- the (data, n, k) -> value contract
+    with explicit errors (``KthError``) instead of in-band sentinels.
+  * ``kselect.dist`` -- the sharded (one process per GPU) replacement of the CGM
+    driver TODO-kth-problem-cgm.c:76-278, with RCCL collectives through
+    torch.distributed.
+
+PyTorch is used only as plumbing (device memory, streams, collectives); every
+selection runs in the HIP kernels of libkth.so.  There is no CPU fallback:
+without the library ``kselect`` fails to import, and without a GPU every
+compute call raises ``KthError(KTH_ENODEV)``.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import (  # noqa: F401
+    KTH_DIST_LEVELS,
+    KTH_EINVAL,
+    KTH_ENODEV,
+    KTH_OK,
+    KTH_PATH_LDS,
+    KTH_PATH_RADIX,
+    KTH_PATH_WINDOW,
+    KTH_PATH_WINDOW_FALLBACK,
+    KTH_ROWS_MAX_COLS,
+    KTH_STATS_WORDS,
+    IntVector,
+    KthError,
+    KthLibraryMissing,
+    KthStats,
+    check,
+    load,
+    strerror,
+)
+
+LIB = load()
+
+# synthetic input families (oracle/kth_oracle.h enum ko_dist)
+UNIFORM_FULL, UNIFORM_HALF, UNIFORM_REF, ALL_EQUAL, FEW_DISTINCT, SORTED_ASC, SORTED_DESC, MOD_1000 = range(8)
+FAMILIES = {
+    "uniform_full": UNIFORM_FULL,
+    "uniform_half": UNIFORM_HALF,
+    "uniform_ref": UNIFORM_REF,
+    "all_equal": ALL_EQUAL,
+    "few_distinct": FEW_DISTINCT,
+    "sorted_asc": SORTED_ASC,
+    "sorted_desc": SORTED_DESC,
+    "mod_1000": MOD_1000,
+}
+DEFAULT_SEED = 0x5EED0001
+
+
+def device_count():
+    return LIB.kth_device_count()
+
+
+def _ptr(x):
+    """Raw address of a torch tensor / numpy array / int."""
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+class Selector:
+    """A kth_ctx: scratch, stream and timing for repeated selections on one GPU."""
+
+    def __init__(self, device=0, stream=None):
+        self._ctx = ctypes.c_void_p()
+        check(LIB.kth_ctx_create(device, ctypes.byref(self._ctx)), "kth_ctx_create")
+        self.device = device
+        if stream is not None:
+            self.set_stream(stream)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if self._ctx:
+            LIB.kth_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def set_stream(self, stream):
+        check(LIB.kth_ctx_set_stream(self._ctx, _stream_handle(stream)), "kth_ctx_set_stream")
+
+    def sync(self):
+        check(LIB.kth_ctx_sync(self._ctx), "kth_ctx_sync")
+
+    def reserve(self, n):
+        check(LIB.kth_ctx_reserve(self._ctx, int(n)), "kth_ctx_reserve")
+
+    # -- selection ---------------------------------------------------------
+    def select(self, keys, k, n=None):
+        """k-th smallest (1-based) of int32 keys (host numpy array or device tensor)."""
+        if n is None:
+            n = keys.numel() if hasattr(keys, "numel") else len(keys)
+        if isinstance(keys, np.ndarray):
+            keys = np.ascontiguousarray(keys, dtype=np.int32)
+        out = ctypes.c_int32()
+        check(LIB.kth_select_i32_ctx(self._ctx, _ptr(keys), int(n), int(k), ctypes.byref(out)),
+              "kth_select_i32_ctx")
+        return out.value
+
+    def select_async(self, d_keys, n, k, d_out):
+        """Enqueue a select of device keys; the answer lands in device int32 *d_out."""
+        check(LIB.kth_select_i32_async(self._ctx, _ptr(d_keys), int(n), int(k), _ptr(d_out)),
+              "kth_select_i32_async")
+
+    def stats(self):
+        st = KthStats()
+        check(LIB.kth_ctx_last_stats(self._ctx, ctypes.byref(st)), "kth_ctx_last_stats")
+        return st.as_dict()
+
+    def rows(self, d_keys, rows, cols, k, d_out, f32=False):
+        fn = LIB.kth_select_rows_f32 if f32 else LIB.kth_select_rows_i32
+        check(fn(self._ctx, _ptr(d_keys), int(rows), int(cols), int(k), _ptr(d_out)), "kth_select_rows")
+
+    def fill(self, d_out, n, family=UNIFORM_FULL, seed=DEFAULT_SEED, param=0, offset=0, n_total=None):
+        if isinstance(family, str):
+            family = FAMILIES[family]
+        if n_total is None:
+            n_total = offset + n
+        check(LIB.kth_fill_synthetic(self._ctx, _ptr(d_out), int(n), int(offset), int(n_total), int(family),
+                                      ctypes.c_uint64(seed), int(param)), "kth_fill_synthetic")
+
+    # -- timing ------------------------------------------------------------
+    def enable_timing(self, on=True):
+        check(LIB.kth_ctx_enable_timing(self._ctx, 1 if on else 0), "kth_ctx_enable_timing")
+
+    def take_timing(self):
+        """(selects, dominant-kernel ms summed, whole-select ms summed) since the last call."""
+        n = ctypes.c_int64()
+        m = ctypes.c_double()
+        t = ctypes.c_double()
+        check(LIB.kth_ctx_take_timing(self._ctx, ctypes.byref(n), ctypes.byref(m), ctypes.byref(t)),
+              "kth_ctx_take_timing")
+        return n.value, m.value, t.value
+
+
+def kth_select(keys, k):
+    """One-shot (data, n, k) -> value: kth_select_i32 (kth-problem-seq.c:32-33)."""
+    if isinstance(keys, np.ndarray):
+        keys = np.ascontiguousarray(keys, dtype=np.int32)
+        n = keys.size
+    else:
+        n = keys.numel()
+    out = ctypes.c_int32()
+    check(LIB.kth_select_i32(_ptr(keys), int(n), int(k), ctypes.byref(out)), "kth_select_i32")
+    return out.value
+
+
+class IntVec:
+    """The reference's IntVector (vector.h:7-11) owned through libkth.so's twin."""
+
+    def __init__(self, capacity):
+        self.p = LIB.VecNew(int(capacity))
+        if not self.p:
+            raise MemoryError("VecNew")
+
+    @classmethod
+    def from_array(cls, a):
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        v = cls(max(1, a.size))
+        ctypes.memmove(v.p.contents.data, a.ctypes.data, a.size * 4)
+        v.p.contents.size = a.size
+        return v
+
+    def add(self, x):
+        return LIB.VecAdd(self.p, int(x))
+
+    def get(self, i):
+        return LIB.VecGet(self.p, int(i))
+
+    def size(self):
+        return LIB.VecGetSize(self.p)
+
+    def array(self):
+        n = self.p.contents.size
+        return np.ctypeslib.as_array(self.p.contents.data, shape=(n,)).copy() if n else np.empty(0, np.int32)
+
+    def quicksort(self):
+        LIB.VecQuickSort(self.p)
+
+    def kth_select(self, k):
+        """VecKthSelect: GPU drop-in for VecQuickSort + VecGet(k-1), VecGet sentinels kept."""
+        return LIB.VecKthSelect(self.p, int(k))
+
+    def kth_select_ex(self, k):
+        out = ctypes.c_int()
+        check(LIB.VecKthSelectEx(self.p, int(k), ctypes.byref(out)), "VecKthSelectEx")
+        return out.value
+
+    def close(self):
+        if self.p:
+            LIB.VecDelete(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

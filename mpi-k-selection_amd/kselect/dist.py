@@ -1,0 +1,120 @@
+"""Sharded exact k-th selection, one process per GPU.
+
+Replaces the CGM driver of the reference (TODO-kth-problem-cgm.c:76-278):
+
+  reference (per round, ~10-12 rounds)           here (once per selection)
+  -------------------------------------          -----------------------------------
+  :103 MPI_Scatterv of 4n bytes from rank 0      shards already resident per GPU
+  :115 local qsort (88% of CGM time)             --
+  :125-131 local median                          local sample (64-key chunks)
+  :135-136 2x MPI_Gather (median, n_i)           all_gather of the samples
+  :139-165 weighted median on rank 0             every rank derives the same window
+  :168 MPI_Bcast of the pivot                    -- (deterministic, no broadcast)
+  :171-185 3-way count L/E/G                     ONE streaming pass per shard
+  :190 MPI_Allreduce(3 ints)                     all_reduce of the counts
+  :194-225 discard via VecErase                  local candidate compaction
+  :242-270 Gather sizes + Barrier + Gatherv      all_reduce of 2048-bin histograms,
+  :277-278 rank-0 qsort + VecGet(k-1)            one per 11-bit digit (3)
+
+Every rank ends with the same answer (the reference prints it on rank 0 only).
+Collectives are ``torch.distributed`` ops -- RCCL over xGMI with the "nccl"
+backend on ROCm, gloo in the CPU tests -- issued on the current stream, so the
+host never waits between steps.  The per-rank device work is a ``backend``:
+``HipBackend`` (libkth.so) in the product; tests plug in a CPU restatement to
+exercise this orchestration on gloo.
+"""
+import torch
+import torch.distributed as dist
+
+from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check
+
+
+def shard_bounds(n, rank, world):
+    """Block partition of TODO-kth-problem-cgm.c:81-100: sizev[i] = n/P + (i < n%P)."""
+    size, rem = divmod(n, world)
+    start = rank * size + min(rank, rem)
+    return start, size + (1 if rank < rem else 0)
+
+
+class HipBackend:
+    """Per-rank device steps through the kth_dist_* entry points of libkth.so."""
+
+    def __init__(self, device, selector=None):
+        self.device = torch.device("cuda", device)
+        self.sel = selector or Selector(device)
+        self.sel.set_stream(torch.cuda.current_stream(self.device))
+        self.ctx = self.sel.handle
+
+    def sample_size(self, n_local):
+        return int(_lib.kth_dist_sample_size(int(n_local)))
+
+    def alloc_slots(self):
+        return torch.zeros((3, KTH_STATS_WORDS), dtype=torch.int64, device=self.device)
+
+    def alloc_sample(self, s):
+        return torch.empty(s, dtype=torch.int32, device=self.device)
+
+    def begin(self, slots, n_total, k):
+        check(_lib.kth_dist_begin(self.ctx, slots.data_ptr(), int(n_total), int(k)), "kth_dist_begin")
+
+    def sample(self, shard, n_local, out, s_local):
+        check(_lib.kth_dist_sample(self.ctx, shard.data_ptr(), int(n_local), out.data_ptr(), int(s_local)),
+              "kth_dist_sample")
+
+    def window(self, sample_all, s_total):
+        check(_lib.kth_dist_window(self.ctx, sample_all.data_ptr(), int(s_total)), "kth_dist_window")
+
+    def scan(self, shard, n_local):
+        r = _lib.kth_dist_scan(self.ctx, shard.data_ptr(), int(n_local))
+        if r < 0:
+            check(r, "kth_dist_scan")
+        return r
+
+    def level(self, shard, n_local, level):
+        r = _lib.kth_dist_level(self.ctx, shard.data_ptr(), int(n_local), int(level))
+        if r < 0:
+            check(r, "kth_dist_level")
+        return r
+
+    def result(self, out):
+        check(_lib.kth_dist_result(self.ctx, out.data_ptr()), "kth_dist_result")
+
+    def alloc_out(self):
+        return torch.empty(1, dtype=torch.int32, device=self.device)
+
+
+class DistSelector:
+    """k-th smallest of the union of every rank's shard (global 1-based k)."""
+
+    def __init__(self, backend, group=None):
+        self.b = backend
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.slots = backend.alloc_slots()
+        self.out = backend.alloc_out()
+        self._sample = None
+        self._gathered = None
+
+    def select(self, shard, n_local, n_total, k):
+        """Enqueue one selection; returns the device (or CPU, for gloo) int32[1] answer tensor.
+
+        n_total must be the sum of n_local over ranks and k in [1, n_total];
+        every rank must pass the same (n_total, k)."""
+        if not (1 <= k <= n_total):
+            raise ValueError(f"k={k} outside [1, {n_total}]")
+        b = self.b
+        s_local = b.sample_size(n_total // self.world)
+        if self._sample is None or self._sample.numel() != s_local:
+            self._sample = b.alloc_sample(s_local)
+            self._gathered = b.alloc_sample(s_local * self.world)
+        b.begin(self.slots, n_total, k)
+        b.sample(shard, n_local, self._sample, s_local)
+        dist.all_gather_into_tensor(self._gathered, self._sample, group=self.group)
+        b.window(self._gathered, s_local * self.world)
+        i = b.scan(shard, n_local)
+        dist.all_reduce(self.slots[i], op=dist.ReduceOp.SUM, group=self.group)
+        for level in range(KTH_DIST_LEVELS):
+            i = b.level(shard, n_local, level)
+            dist.all_reduce(self.slots[i], op=dist.ReduceOp.SUM, group=self.group)
+        b.result(self.out)
+        return self.out

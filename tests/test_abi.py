@@ -1,0 +1,161 @@
+"""CPU checks of the drop-in boundary: libkth.so loads, exports every entry
+point declared in include/*.h, keeps the reference IntVector ABI and host
+semantics, and has no CPU fallback (compute calls fail loudly without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+LIB = os.path.join(PKG, "lib", "libkth.so")
+REF_VEC = os.path.join(REPO, "oracle", "_ref", "libvector_ref.so")
+
+
+def declared_functions(header):
+    text = open(os.path.join(REPO, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"#define[^\n]*", "", text)
+    names = re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", text)
+    return sorted({n for n in names if n not in ("sizeof",)})
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import kselect
+    return kselect.LIB
+
+
+def test_headers_declare_expected_api():
+    k = declared_functions("kth.h")
+    v = declared_functions("vector.h")
+    for name in ("kth_select_i32", "kth_select_i32_async", "kth_ctx_create", "kth_select_rows_f32",
+                 "kth_dist_scan", "kth_dist_level", "kth_dist_result"):
+        assert name in k
+    # the reference's 18 prototypes (vector.h:13-33) + the drop-in select
+    ref18 = ["VecNew", "VecAdd", "VecDelete", "VecErase", "MinFind", "MaxFind", "AverageFind", "VecGetCapacity",
+             "VecGetSize", "VecIsFull", "VecSet", "VecGet", "VecSearch", "VecQuickSort", "VecQuickSort2",
+             "VecBinarySearch", "VecBinarySearch2"]
+    assert len(ref18) == 17  # the reference header has 17 functions + the struct
+    for name in ref18 + ["VecKthSelect", "VecKthSelectEx"]:
+        assert name in v, name
+
+
+def test_library_exports_every_declared_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for h in ("kth.h", "vector.h"):
+        for name in declared_functions(h):
+            assert name in exported, f"{name} declared in include/{h} but not exported by libkth.so"
+
+
+def test_python_binding_covers_every_symbol():
+    from kselect._lib import PROTOS
+    for h in ("kth.h", "vector.h"):
+        for name in declared_functions(h):
+            assert name in PROTOS, name
+
+
+def test_intvector_layout():
+    from kselect import IntVector
+    assert ctypes.sizeof(IntVector) == 16
+    assert IntVector.size.offset == 0 and IntVector.capacity.offset == 4 and IntVector.data.offset == 8
+
+
+def test_no_cpu_fallback(lib):
+    """Without a GPU every compute entry point fails loudly (KTH_ENODEV)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import kselect
+    a = np.arange(100, dtype=np.int32)
+    out = ctypes.c_int32(12345)
+    assert lib.kth_select_i32(a.ctypes.data, 100, 50, ctypes.byref(out)) == kselect.KTH_ENODEV
+    assert out.value == 12345
+    with pytest.raises(kselect.KthError):
+        kselect.Selector(0)
+    v = kselect.IntVec.from_array(a)
+    assert v.kth_select(5) == -3  # VecKthSelect's device-error sentinel
+
+
+def test_missing_library_is_loud():
+    code = ("import sys; sys.path.insert(0, %r); import kselect" % PKG)
+    p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, KTH_LIB="/nonexistent/libkth.so"),
+                       capture_output=True, text=True)
+    assert p.returncode != 0 and "KthLibraryMissing" in p.stderr
+
+
+def _vec_ops(L, seed):
+    """Random IntVector op sequence (no sort); returns the observable trace."""
+    L.VecNew.restype = ctypes.c_void_p
+    for name in ("VecAdd", "VecErase", "MinFind", "VecGetCapacity", "VecGetSize", "VecIsFull", "VecSet",
+                 "VecGet", "VecSearch"):
+        getattr(L, name).restype = ctypes.c_int
+    L.AverageFind.restype = ctypes.c_double
+    rng = np.random.default_rng(seed)
+    v = ctypes.c_void_p(L.VecNew(4))
+    trace = []
+    for _ in range(400):
+        op = rng.integers(0, 8)
+        x = int(rng.integers(-1000, 1000))
+        i = int(rng.integers(-2, 40))
+        if op <= 2:
+            trace.append(("add", L.VecAdd(v, x)))
+        elif op == 3:
+            trace.append(("erase", L.VecErase(v, i)))
+        elif op == 4:
+            trace.append(("set", L.VecSet(v, i, x)))
+        elif op == 5:
+            trace.append(("get", L.VecGet(v, i)))
+        elif op == 6:
+            trace.append(("search", L.VecSearch(v, i, x)))
+        else:
+            trace.append(("stat", L.VecGetSize(v), L.VecIsFull(v), L.MinFind(v), L.AverageFind(v)))
+    n = L.VecGetSize(v)
+    trace.append(("final", [L.VecGet(v, j) for j in range(n)]))
+    L.VecDelete(v)
+    return trace
+
+
+def test_intvector_semantics_match_reference():
+    """Same observable behaviour as the reference vector.c on random op
+    sequences (compiled from /root/reference into oracle/_ref)."""
+    if not os.path.exists(REF_VEC):
+        pytest.skip("oracle/_ref not built")
+    ours = ctypes.CDLL(LIB)
+    ref = ctypes.CDLL(REF_VEC)
+    for seed in range(5):
+        assert _vec_ops(ours, seed) == _vec_ops(ref, seed)
+
+
+def test_quicksort_fixes_reference_comparator():
+    """VecQuickSort sorts full-range keys; the reference's `*a - *b` does not."""
+    import kselect
+    rng = np.random.default_rng(1)
+    a = rng.integers(-2 ** 31, 2 ** 31, size=4096, dtype=np.int64).astype(np.int32)
+    v = kselect.IntVec.from_array(a)
+    v.quicksort()
+    np.testing.assert_array_equal(v.array(), np.sort(a))
+    if os.path.exists(REF_VEC):
+        ref = ctypes.CDLL(REF_VEC)
+        from kselect import IntVector
+        b = a.copy()
+        iv = IntVector(b.size, b.size, b.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        ref.VecQuickSort(ctypes.byref(iv))
+        assert not np.array_equal(b, np.sort(a))  # the documented reference defect
+
+
+def test_reference_driver_links_against_twin(tmp_path):
+    """The reference's unmodified kth-problem-seq.c compiles and links against
+    include/vector.h + libkth.so (ABI drop-in)."""
+    src = "/root/reference/kth-problem-seq.c"
+    if not os.path.exists(src):
+        pytest.skip("reference not present")
+    exe = tmp_path / "seq_on_twin"
+    subprocess.run(["gcc", "-O2", "-w", "-I", os.path.join(REPO, "include"), src, "-L", os.path.dirname(LIB),
+                    "-lkth", "-o", str(exe)], check=True)
+    assert exe.exists()
