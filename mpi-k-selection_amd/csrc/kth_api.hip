@@ -29,7 +29,10 @@ constexpr int64_t RADIX_MAX_N = 1ll << 22;   // radix path up to here, window pa
 constexpr int64_t SAMPLE_MAX = 1ll << 20;    // sample keys (single GPU / total over ranks)
 constexpr double WINDOW_Z = 6.0;             // window half-width in sample standard deviations
 constexpr int LEVEL_GRID_MAX = 1024;
-constexpr int GATHER_CHUNKS_PER_WAVE = 16;
+int gather_grid(u64 nchunks) {
+    const u64 per_wg = (u64)(kth::DENSE_BLK / kth::WAVE) * kth::GATHER_BATCH;  // chunks per workgroup round
+    return (int)std::max<u64>(1, (nchunks + per_wg - 1) / per_wg);
+}
 constexpr size_t ISLOT_WORDS = 3 * (size_t)kth::STATS_WORDS + 2;  // 3 slots + cand_count + pad
 constexpr int MAX_EVENTS = 4 * 2048;
 
@@ -52,6 +55,7 @@ constexpr int MAX_EVENTS = 4 * 2048;
 
 struct kth_ctx {
     int device = 0;
+    int main_grid = 0;  // streaming-pass workgroups (num_cu * 8; KTH_MAIN_WG_PER_CU overrides)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -147,7 +151,6 @@ void ev_mark(kth_ctx *c, std::vector<hipEvent_t> &pool, int &used) {
     (void)hipEventRecord(pool[used++], c->stream);
 }
 void ev_main(kth_ctx *c) { ev_mark(c, c->ev_main, c->main_used); }
-void ev_total(kth_ctx *c) { ev_mark(c, c->ev_total, c->total_used); }
 
 int launch_check() {
     hipError_t e = hipGetLastError();
@@ -158,9 +161,26 @@ int launch_check() {
     return KTH_OK;
 }
 
-int level_grid(u64 count) {
-    u64 g = (count + kth::LEVEL_MIN_PER_WG - 1) / kth::LEVEL_MIN_PER_WG;
+// Histogram levels.  Dense levels (every key of the domain lands in the
+// histogram: the first digit of a domain) run few 1024-thread workgroups of
+// DENSE_PER_WG keys, so at most ~domain/DENSE_PER_WG workgroups add to each
+// global bin; sparse levels (only keys matching the prefix) run many small ones.
+constexpr u64 DENSE_PER_WG = 1ull << 16;
+constexpr u64 SPARSE_PER_WG = (u64)kth::BLK * kth::LEVEL_UNROLL * 4;
+
+int level_grid(u64 count, u64 per_wg) {
+    u64 g = (count + per_wg - 1) / per_wg;
     return (int)std::max<u64>(1, std::min<u64>(LEVEL_GRID_MAX, g));
+}
+
+void launch_level(kth_ctx *c, StepArgs a, bool dense, int grid) {
+    if (dense) {
+        a.min_per_wg = DENSE_PER_WG;
+        kth::k_level<kth::DENSE_BLK><<<grid, kth::DENSE_BLK, 0, c->stream>>>(a);
+    } else {
+        a.min_per_wg = SPARSE_PER_WG;
+        kth::k_level<kth::BLK><<<grid, kth::BLK, 0, c->stream>>>(a);
+    }
 }
 
 // ---------------------------------------------------------------- paths
@@ -174,23 +194,22 @@ int run_small(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
 }
 
 int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
-    const int g = level_grid((u64)n);
     StepArgs a = step(c, kth::ADV_INIT_FULL, -1, 0, nullptr, islot(c, 1), islot(c, 2));
     a.keys = keys;
     a.n_local = (u64)n;
     a.init_n = (u64)n;
     a.init_k = (u64)k;
     ev_main(c);  // the first radix pass is the dominant kernel here
-    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, true, level_grid((u64)n, DENSE_PER_WG));
     ev_main(c);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.keys = keys;
     a.n_local = (u64)n;
-    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, level_grid((u64)n, SPARSE_PER_WG));
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
     a.keys = keys;
     a.n_local = (u64)n;
-    kth::k_level<<<g, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, level_grid((u64)n, SPARSE_PER_WG));
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), nullptr, nullptr);
     kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
     c->last_state = 1;
@@ -216,40 +235,38 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.init_s = (u64)s;
     a.r_lo = r_lo;
     a.r_hi = r_hi;
-    const u64 waves = (nchunks + GATHER_CHUNKS_PER_WAVE - 1) / GATHER_CHUNKS_PER_WAVE;
-    const int gg = (int)std::max<u64>(1, (waves + (kth::BLK / kth::WAVE) - 1) / (kth::BLK / kth::WAVE));
-    kth::k_gather<true><<<gg, kth::BLK, 0, c->stream>>>(a, keys, stride, c->sample, (u64)s);
-    // digits 2, 3 of the sample ranks
-    const int gs = level_grid((u64)s);
+    kth::k_gather<true><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, keys, stride, c->sample, (u64)s);
+    // digits 2, 3 of the sample ranks (sparse: only keys in the picked bins)
+    const int gs = level_grid((u64)s, SPARSE_PER_WG);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.sample = c->sample;
     a.sample_count = (u64)s;
-    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, gs);
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
     a.sample = c->sample;
     a.sample_count = (u64)s;
-    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, gs);
     // the streaming pass
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), islot(c, 1), islot(c, 2));
     a.keys = keys;
     a.n_local = (u64)n;
     ev_main(c);
-    kth::k_main<<<c->num_cu * 8, kth::BLK, 0, c->stream>>>(a, c->cand);
+    kth::k_main<<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand);
     ev_main(c);
-    // decide + candidate (or fallback) levels
-    const int gl = LEVEL_GRID_MAX;
+    // decide + candidate (or fallback) levels.  The grids cover the fallback
+    // (whole input); in the common case only the WGs the candidates need run.
     a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), islot(c, 2), islot(c, 0));
     a.keys = keys;
     a.n_local = (u64)n;
-    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, true, LEVEL_GRID_MAX);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 2), islot(c, 0), islot(c, 1));
     a.keys = keys;
     a.n_local = (u64)n;
-    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, LEVEL_GRID_MAX);
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 0), islot(c, 1), islot(c, 2));
     a.keys = keys;
     a.n_local = (u64)n;
-    kth::k_level<<<gl, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, LEVEL_GRID_MAX);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), nullptr, nullptr);
     kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
     c->last_state = 1;
@@ -263,7 +280,6 @@ int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_
         HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
         c->dirty = false;
     }
-    ev_total(c);
     int rc;
     if (n <= SMALL_N)
         rc = run_small(c, d_keys, n, k, d_out, d_status);
@@ -271,7 +287,6 @@ int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_
         rc = run_radix(c, d_keys, n, k, d_out, d_status);
     else
         rc = run_window(c, d_keys, n, k, d_out, d_status);
-    ev_total(c);
     if (rc != KTH_OK) c->dirty = true;
     return rc;
 }
@@ -330,6 +345,27 @@ int kth_ctx_create(int device, kth_ctx **out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             c->num_cu = prop.multiProcessorCount;
+        {
+            // One resident wave of workgroups: every WG streams an equal share
+            // and no tail of late WGs.  Residency from k_main's own VGPR and LDS
+            // use (4 waves per 256-thread WG = one per SIMD; a SIMD holds
+            // 512 / alloc(VGPR) waves, MI355X_MICROARCH.md register files).
+            // hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports here.
+            int per = 4;
+            hipFuncAttributes fa;
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kth::k_main)) == hipSuccess &&
+                fa.numRegs > 0) {
+                const int alloc = (fa.numRegs + 7) / 8 * 8;
+                const int by_vgpr = std::min(8, 512 / alloc);
+                const int lds = (int)fa.sharedSizeBytes;
+                const int by_lds = lds > 0 ? (160 * 1024) / lds : 8;
+                per = std::max(1, std::min(by_vgpr, by_lds));
+            }
+            (void)hipGetLastError();
+            const char *e = getenv("KTH_MAIN_WG_PER_CU");
+            if (e) per = std::max(1, atoi(e));
+            c->main_grid = c->num_cu * per;
+        }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
         if (hipMalloc(reinterpret_cast<void **>(&c->st), 2 * sizeof(SelState)) != hipSuccess ||
@@ -578,9 +614,8 @@ int kth_dist_sample(kth_ctx *c, const int32_t *d_keys, int64_t n_local, uint32_t
     const u64 stride = (u64)n_local / nchunks;
     StepArgs a;
     memset(&a, 0, sizeof a);
-    const u64 waves = (nchunks + GATHER_CHUNKS_PER_WAVE - 1) / GATHER_CHUNKS_PER_WAVE;
-    const int gg = (int)std::max<u64>(1, (waves + 3) / 4);
-    kth::k_gather<false><<<gg, kth::BLK, 0, c->stream>>>(a, d_keys, stride, d_sample, (u64)s_local);
+    kth::k_gather<false><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, d_keys, stride, d_sample,
+                                                                                (u64)s_local);
     return launch_check();
 }
 
@@ -589,7 +624,6 @@ int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
     KTH_TRY(set_device(c));
     u64 r_lo, r_hi;
     window_ranks(c->dist_n, c->dist_k, s_total, &r_lo, &r_hi);
-    const int gs = level_grid((u64)s_total);
     StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
     a.init_n = (u64)c->dist_n;
     a.init_k = (u64)c->dist_k;
@@ -598,15 +632,16 @@ int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
     a.r_hi = r_hi;
     a.sample = d_sample;
     a.sample_count = (u64)s_total;
-    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, true, level_grid((u64)s_total, DENSE_PER_WG));
+    const int gs = level_grid((u64)s_total, SPARSE_PER_WG);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.sample = d_sample;
     a.sample_count = (u64)s_total;
-    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, gs);
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
     a.sample = d_sample;
     a.sample_count = (u64)s_total;
-    kth::k_level<<<gs, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, false, gs);
     return launch_check();
 }
 
@@ -618,7 +653,7 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
-    kth::k_main<<<c->num_cu * 8, kth::BLK, 0, c->stream>>>(a, c->cand);
+    kth::k_main<<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand);
     ev_main(c);
     c->dist_level_next = 0;
     KTH_TRY(launch_check());
@@ -637,7 +672,7 @@ int kth_dist_level(kth_ctx *c, const int32_t *d_keys, int64_t n_local, int level
                       level == 0 ? nullptr : U[zero]);
     a.keys = d_keys;
     a.n_local = (u64)n_local;
-    kth::k_level<<<LEVEL_GRID_MAX, kth::BLK, 0, c->stream>>>(a);
+    launch_level(c, a, level == 0, LEVEL_GRID_MAX);
     KTH_TRY(launch_check());
     c->dist_level_next = level + 1;
     return acc;

@@ -151,4 +151,40 @@ __device__ bool block_pick(H hist, int nb, u64 k, uint32_t *out_bin, u64 *out_be
     return ok;
 }
 
+
+// block_pick over values the caller already holds: thread t owns bins
+// [t*PER, t*PER + PER) of an (NB = BLOCK*PER)-bin histogram.  Lets a kernel
+// issue its histogram loads together with its other loads.
+template <int BLOCK, int PER>
+__device__ bool block_pick_vals(const u64 (&h)[PER], u64 k, uint32_t *out_bin, u64 *out_below, u64 *scratch) {
+    u64 sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) sum += h[j];
+    u64 total;
+    const u64 pre = block_exclusive_scan<BLOCK>(sum, scratch, &total);
+    u64 *res = scratch + BLOCK / WAVE;
+    if (threadIdx.x == 0) res[0] = 0;
+    __syncthreads();
+    if (k >= 1 && k > pre && k <= pre + sum) {
+        u64 cum = pre;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (!found && cum + h[j] >= k) {
+                res[0] = 1;
+                res[1] = (u64)(threadIdx.x * PER + j);
+                res[2] = cum;
+                found = true;
+            }
+            cum += h[j];
+        }
+    }
+    __syncthreads();
+    const bool ok = res[0] != 0;
+    *out_bin = (uint32_t)res[1];
+    *out_below = res[2];
+    __syncthreads();
+    return ok;
+}
+
 }  // namespace kth

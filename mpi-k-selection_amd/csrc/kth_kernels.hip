@@ -16,15 +16,19 @@
 // Replaces the CGM rounds of TODO-kth-problem-cgm.c:122-233 (local median,
 // weighted median, 3-way count, discard) and the final solve :235-278; and the
 // qsort + VecGet of kth-problem-seq.c:32-33.
+#include <type_traits>
+
 #include "kth_device.hpp"
 
 namespace kth {
 
 constexpr int BLK = 256;
-constexpr int MAIN_UNROLL = 4;
-constexpr int LBUF = 4096;            // per-workgroup candidate staging (16 KiB LDS)
-constexpr u64 LEVEL_MIN_PER_WG = 1ull << 14;
+constexpr int MAIN_UNROLL = 8;       // 16-B loads in flight per thread in k_main
+constexpr int WREG = 1024;            // per-wave candidate staging region (4 KiB LDS)
+constexpr int LEVEL_UNROLL = 8;       // 16-B loads in flight per thread in k_level
+constexpr int DENSE_BLK = 1024;       // workgroup size of the dense-histogram levels
 constexpr int SAMPLE_CHUNK = 64;      // keys per sampled chunk = one wave's 256-B load
+constexpr int GATHER_BATCH = 16;      // sampled chunks in flight per wave
 constexpr int SMALL_BLOCK = 1024;
 constexpr int ROWS_BLOCK = 256;
 
@@ -51,6 +55,7 @@ struct StepArgs {
     u64 n_local;
     int adv;
     u64 init_n, init_k, init_s, r_lo, r_hi;
+    u64 min_per_wg;        // keys per active workgroup (sets how many WGs flush a histogram)
 };
 
 // ------------------------------------------------------------- the advance
@@ -107,6 +112,19 @@ __device__ __forceinline__ void decide(SelState &s, const u64 *c) {
 
 template <int BLOCK>
 __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
+    // Histogram words are loaded by every thread up front, in parallel with the
+    // state: a digit has at most NBINS bins and bins past 2^d are zero in a
+    // zeroed slot, so picking over all NBINS is exact for any digit width.
+    constexpr int PER = NBINS / BLOCK;
+    u64 h0[PER], h1[PER];
+    if (a.adv == ADV_PICK) {
+        const u64 *b0 = a.stats_in + NCOUNTS + threadIdx.x * PER;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            h0[j] = b0[j];
+            h1[j] = b0[NBINS + j];
+        }
+    }
     if (threadIdx.x == 0) {
         if (a.adv == ADV_INIT_SAMPLE || a.adv == ADV_INIT_FULL) {
             SelState s;
@@ -145,13 +163,12 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
                               ss.t[t].active && ss.t[t].done < ss.W;
             if (!need) continue;  // block-uniform: read from LDS after a barrier
             const uint32_t d = digit_bits(ss.W, ss.t[t].done);
-            const int src = (t == 1 && ss.share) ? 0 : t;
-            const u64 *h = a.stats_in + NCOUNTS + src * NBINS;
+            const bool use0 = t == 0 || ss.share;
             uint32_t bin;
             u64 below;
-            const bool ok = block_pick<BLOCK>([&](int i) { return h[i]; }, 1 << d, ss.t[t].k, &bin, &below, scratch);
+            const bool ok = block_pick_vals<BLOCK, PER>(use0 ? h0 : h1, ss.t[t].k, &bin, &below, scratch);
             if (threadIdx.x == 0) {
-                if (!ok) {
+                if (!ok || bin >= (1u << d)) {
                     ss.error = 1 + t;
                     ss.mode = MODE_DONE;
                 } else {
@@ -168,15 +185,20 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
 }
 
 // ----------------------------------------------------------------- streaming
-// Visit n 32-bit words at p (4-byte aligned) as keys, f(key, valid).  Calls
-// are wave-convergent (every lane calls f the same number of times; `valid`
-// masks the lanes past the end), so f may use ballots.  Block-contiguous tiles
-// of BLOCK * UNROLL 16-byte vectors, grid-strided.  XOR flips the sign bit
-// (int32 -> order-preserving uint32).
+// Visit n 32-bit words at p (4-byte aligned) as keys, one TILE per thread at a
+// time: f(keys[4 * UNROLL], valid_mask), key j of a thread's tile being
+// component j % 4 of its (j / 4)-th 16-byte vector.  Calls are wave-convergent
+// (every lane calls f the same number of times; invalid keys are masked off),
+// so f may use ballots and shuffles.  Block-contiguous tiles of BLOCK * UNROLL
+// 16-byte vectors (each wave-instruction reads 1 KiB contiguous), grid-strided;
+// all UNROLL loads of a tile are issued before any is used.  XOR flips the sign
+// bit (int32 -> order-preserving uint32).
 template <int BLOCK, int UNROLL, bool XOR, typename F>
-__device__ __forceinline__ void stream_keys(const uint32_t *__restrict__ p, u64 n, uint32_t wg, uint32_t nwg,
-                                            F &&f) {
-    const uint32_t X = XOR ? 0x80000000u : 0u;
+__device__ __forceinline__ void stream_tiles(const uint32_t *__restrict__ p, u64 n, uint32_t wg, uint32_t nwg,
+                                             F &&f) {
+    constexpr uint32_t X = XOR ? 0x80000000u : 0u;
+    constexpr int K = 4 * UNROLL;
+    static_assert(K <= 32, "valid mask is 32 bits");
     const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
     u64 head = ((16u - (uint32_t)(addr & 15u)) & 15u) >> 2;
     if (head > n) head = n;
@@ -184,37 +206,43 @@ __device__ __forceinline__ void stream_keys(const uint32_t *__restrict__ p, u64 
     const u64 nv = (n - head) >> 2;
     const u64 tail0 = head + (nv << 2);
     const u64 tile = (u64)BLOCK * UNROLL;
+    uint32_t k[K];
     for (u64 t0 = (u64)wg * tile; t0 < nv; t0 += (u64)nwg * tile) {
         uint4 x[UNROLL];
+        uint32_t valid = 0xFFFFFFFFu;
         if (t0 + tile <= nv) {
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) x[u] = load_nt(&v[t0 + u * BLOCK + threadIdx.x]);
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                f(x[u].x ^ X, true);
-                f(x[u].y ^ X, true);
-                f(x[u].z ^ X, true);
-                f(x[u].w ^ X, true);
-            }
         } else {
+            valid = 0;
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 const u64 i = t0 + u * BLOCK + threadIdx.x;
                 const bool ok = i < nv;
                 x[u] = ok ? v[i] : make_uint4(0, 0, 0, 0);
-                f(x[u].x ^ X, ok);
-                f(x[u].y ^ X, ok);
-                f(x[u].z ^ X, ok);
-                f(x[u].w ^ X, ok);
+                valid |= ok ? (0xFu << (4 * u)) : 0u;
             }
         }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            k[4 * u + 0] = x[u].x ^ X;
+            k[4 * u + 1] = x[u].y ^ X;
+            k[4 * u + 2] = x[u].z ^ X;
+            k[4 * u + 3] = x[u].w ^ X;
+        }
+        if (valid == 0xFFFFFFFFu)
+            f(k, valid, std::true_type{});
+        else
+            f(k, valid, std::false_type{});
     }
-    if (wg == 0) {  // ragged head and tail: < 4 keys each
+    if (wg == 0) {  // ragged head and tail: < 4 keys each, one tile
         const u64 j = threadIdx.x;
         const bool okh = j < head, okt = j < n - tail0;
-        const uint32_t xh = okh ? p[j] : 0u, xt = okt ? p[tail0 + j] : 0u;
-        f(xh ^ X, okh);
-        f(xt ^ X, okt);
+#pragma unroll
+        for (int i = 0; i < K; ++i) k[i] = 0;
+        k[0] = (okh ? p[j] : 0u) ^ X;
+        k[1] = (okt ? p[tail0 + j] : 0u) ^ X;
+        f(k, (okh ? 1u : 0u) | (okt ? 2u : 0u), std::false_type{});
     }
 }
 
@@ -281,11 +309,12 @@ __device__ __forceinline__ void publish(const SelState &ss, uint32_t share, cons
 
 // One radix level: advance, then histogram the next digit of every
 // unresolved target over the current domain (sample / candidates / input).
-__global__ __launch_bounds__(BLK) void k_level(StepArgs a) {
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     __shared__ SelState ss;
-    __shared__ u64 scratch[BLK / WAVE + 4];
+    __shared__ u64 scratch[BLOCK / WAVE + 4];
     __shared__ uint32_t lh[2][NBINS];
-    advance<BLK>(ss, a, scratch);
+    advance<BLOCK>(ss, a, scratch);
     bool share;
     const HistPlan plan = make_plan(ss, &share);
     const uint32_t mode = ss.mode;
@@ -295,60 +324,146 @@ __global__ __launch_bounds__(BLK) void k_level(StepArgs a) {
         else if (mode == MODE_CAND) count = min(*a.cand_count, a.cap);
         else if (mode == MODE_FULL) count = a.n_local;
     }
-    publish<BLK>(ss, share, a);
-    const u64 want = (count + LEVEL_MIN_PER_WG - 1) / LEVEL_MIN_PER_WG;
+    publish<BLOCK>(ss, share, a);
+    // Few workgroups per histogram keeps the number of same-address global
+    // atomics per bin (the flush's serialisation) low; min_per_wg is the host's
+    // choice per level (dense levels: large).
+    const u64 want = (count + a.min_per_wg - 1) / a.min_per_wg;
     const uint32_t active = (uint32_t)min((u64)gridDim.x, want);
     if (blockIdx.x >= active) return;
-    for (int i = threadIdx.x; i < 2 * NBINS; i += BLK) (&lh[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 2 * NBINS; i += BLOCK) (&lh[0][0])[i] = 0;
     __syncthreads();
-    auto f = [&](uint32_t key, bool ok) { hist_add<BLK>(lh, plan, key, ok); };
+    auto f = [&](const uint32_t *k, uint32_t valid, auto full) {
+#pragma unroll
+        for (int j = 0; j < 4 * LEVEL_UNROLL; ++j)
+            hist_add<BLOCK>(lh, plan, k[j], decltype(full)::value || ((valid >> j) & 1u));
+    };
     if (mode == MODE_FULL)
-        stream_keys<BLK, 4, true>(reinterpret_cast<const uint32_t *>(a.keys), count, blockIdx.x, active, f);
+        stream_tiles<BLOCK, LEVEL_UNROLL, true>(reinterpret_cast<const uint32_t *>(a.keys), count, blockIdx.x, active,
+                                                f);
     else
-        stream_keys<BLK, 4, false>(mode == MODE_SAMPLE ? a.sample : a.cand, count, blockIdx.x, active, f);
-    hist_flush<BLK>(lh, plan, a.stats_acc);
+        stream_tiles<BLOCK, LEVEL_UNROLL, false>(mode == MODE_SAMPLE ? a.sample : a.cand, count, blockIdx.x, active,
+                                                 f);
+    hist_flush<BLOCK>(lh, plan, a.stats_acc);
 }
 
 // Sample gather: s keys in chunks of 64 contiguous keys spread evenly over the
 // shard (stride = chunk distance in keys).  With FUSE the first digit's
 // histogram of the sample is built too (single-GPU: the sample is complete).
 template <bool FUSE>
-__global__ __launch_bounds__(BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 stride,
+__global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 stride,
                                                 uint32_t *__restrict__ sample, u64 s) {
     __shared__ SelState ss;
-    __shared__ u64 scratch[BLK / WAVE + 4];
+    __shared__ u64 scratch[DENSE_BLK / WAVE + 4];
     __shared__ uint32_t lh[2][NBINS];
     HistPlan plan;
     bool share = false;
     if (FUSE) {
-        advance<BLK>(ss, a, scratch);
+        advance<DENSE_BLK>(ss, a, scratch);
         plan = make_plan(ss, &share);
-        publish<BLK>(ss, share, a);
-        for (int i = threadIdx.x; i < 2 * NBINS; i += BLK) (&lh[0][0])[i] = 0;
+        publish<DENSE_BLK>(ss, share, a);
+        for (int i = threadIdx.x; i < 2 * NBINS; i += DENSE_BLK) (&lh[0][0])[i] = 0;
         __syncthreads();
     }
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nchunks = s / SAMPLE_CHUNK;
-    const u64 gw = ((u64)blockIdx.x * BLK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (BLK / WAVE);
-    for (u64 c = gw; c < nchunks; c += nw) {
-        const uint32_t key = key_of_i32((uint32_t)keys[c * stride + lane]);
-        sample[c * SAMPLE_CHUNK + lane] = key;
-        if (FUSE) hist_add<BLK>(lh, plan, key, true);
+    const u64 gw = ((u64)blockIdx.x * DENSE_BLK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (DENSE_BLK / WAVE);
+    // every wave owns GATHER_BATCH consecutive chunk slots per round; all loads
+    // of a round are in flight together (the chunks are 256 KiB apart in HBM)
+    for (u64 c0 = gw * GATHER_BATCH; c0 < nchunks; c0 += nw * GATHER_BATCH) {
+        uint32_t kk[GATHER_BATCH];
+#pragma unroll
+        for (int j = 0; j < GATHER_BATCH; ++j) {
+            const u64 c = c0 + j;
+            kk[j] = c < nchunks ? key_of_i32((uint32_t)keys[c * stride + lane]) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < GATHER_BATCH; ++j) {
+            const u64 c = c0 + j;
+            if (c < nchunks) {
+                sample[c * SAMPLE_CHUNK + lane] = kk[j];
+                if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j], true);
+            }
+        }
     }
-    if (FUSE) hist_flush<BLK>(lh, plan, a.stats_acc);
+    if (FUSE) hist_flush<DENSE_BLK>(lh, plan, a.stats_acc);
 }
 
 // The streaming pass.  Window [lo, hi] comes from the advance (last sample
-// digit).  Per key: #<lo, #==lo, #==hi in registers; keys strictly inside the
-// window are compacted through an LDS buffer (one LDS atomic per wave-key
-// group that has any, one global reservation per workgroup).
+// digit).  Per key: #<lo, #==lo, #==hi in registers.  Keys strictly inside the
+// window are marked in a per-thread bit mask per tile; one wave-wide scan of the
+// per-lane counts places them in the wave's private LDS region (no LDS atomics,
+// no barriers).  A wave flushes its region to the candidate buffer itself, with
+// one global reservation, whenever the next tile might not fit -- so staging
+// never overflows however many keys a workgroup streams.  A single tile with
+// more than WREG candidates (over half its keys inside the window: adversarial
+// input only) is written straight to HBM.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+    const int lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, WAVE);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// Reserve `cnt` slots of the candidate buffer for one wave (lane WAVE-1 does the
+// atomic); flags the per-rank overflow word exactly once, on the crossing.
+__device__ __forceinline__ u64 reserve_cands(u64 *cand_count, u64 *acc, u64 cap, uint32_t cnt) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    u64 g = 0;
+    if (lane == WAVE - 1) {
+        g = atomicAdd(cand_count, (u64)cnt);
+        if (g <= cap && g + cnt > cap) atomicAdd(&acc[C_OVF], 1ull);
+    }
+    return __shfl(g, WAVE - 1, WAVE);
+}
+
+// Per-tile candidate handling shared by full and ragged tiles.  `cm` has bit j
+// set for key j of this lane's tile inside the window.  One wave scan places
+// the wave's candidates at the end of its LDS region (flushed first if they
+// might not fit); predicated LDS stores write them.
+template <int K>
+__device__ __forceinline__ void stage_tile(const uint32_t (&kk)[K], uint32_t cm, uint32_t *reg, uint32_t &wfill,
+                                           u64 &winside, u64 *cand_count, u64 *acc, u64 cap,
+                                           uint32_t *__restrict__ cand_out) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const uint32_t c = (uint32_t)__popc(cm);
+    const uint32_t incl = wave_inclusive_scan(c);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, WAVE - 1);
+    winside += total;
+    if (wfill + total > (uint32_t)WREG) {  // wave-uniform: flush this wave's region
+        __builtin_amdgcn_wave_barrier();
+        const u64 g = reserve_cands(cand_count, acc, cap, wfill);
+        for (uint32_t i = lane; i < wfill; i += WAVE)
+            if (g + i < cap) cand_out[g + i] = reg[i];
+        __builtin_amdgcn_wave_barrier();
+        wfill = 0;
+    }
+    if (total > (uint32_t)WREG) {  // adversarial tile (> half its keys inside): straight to HBM
+        u64 g = reserve_cands(cand_count, acc, cap, total) + (incl - c);
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (cm & (1u << j)) {
+                if (g < cap) cand_out[g] = kk[j];
+                ++g;
+            }
+        return;
+    }
+    uint32_t pos = wfill + incl - c;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (cm & (1u << j)) reg[pos++] = kk[j];
+    wfill += total;
+}
+
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out) {
+    constexpr int U = MAIN_UNROLL, K = 4 * U;
     __shared__ SelState ss;
     __shared__ u64 scratch[BLK / WAVE + 4];
-    __shared__ uint32_t lbuf[LBUF];
-    __shared__ uint32_t lcount;
-    __shared__ u64 red[3][BLK / WAVE];
-    __shared__ u64 gbase;
+    __shared__ uint32_t region[BLK / WAVE][WREG];
+    __shared__ u64 red[4][BLK / WAVE];
     advance<BLK>(ss, a, scratch);
     publish<BLK>(ss, 0, a);
     if (ss.mode != MODE_MAIN) return;  // block-uniform (error or resolved)
@@ -356,45 +471,99 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     const u64 cap = a.cap;
     u64 *const cand_count = a.cand_count;
     u64 *const acc = a.stats_acc;
-    if (threadIdx.x == 0) lcount = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & (WAVE - 1);
-    uint32_t clt = 0, ceqlo = 0, ceqhi = 0;
-    stream_keys<BLK, MAIN_UNROLL, true>(
-        reinterpret_cast<const uint32_t *>(a.keys), a.n_local, blockIdx.x, gridDim.x, [&](uint32_t u, bool ok) {
-            clt += (ok & (u < lo)) ? 1u : 0u;
-            ceqlo += (ok & (u == lo)) ? 1u : 0u;
-            ceqhi += (ok & (u == hi)) ? 1u : 0u;
-            const bool in = ok & (u > lo) & (u < hi);
-            const u64 m = __ballot(in);
-            if (m) {
-                const uint32_t cnt = (uint32_t)__popcll(m);
-                const uint32_t rank =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                const int leader = __ffsll((long long)m) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&lcount, cnt);
-                base = __shfl(base, leader, WAVE);
-                const uint32_t pos = base + rank;
-                if (in && pos < LBUF) lbuf[pos] = u;
-                if (base + cnt > LBUF) {  // staging full: this group goes straight to HBM
-                    const bool spill = in && pos >= LBUF;
-                    const u64 ms = __ballot(spill);
-                    const uint32_t cs = (uint32_t)__popcll(ms);
-                    const uint32_t rs =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(ms >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ms, 0u));
-                    const int l2 = __ffsll((long long)ms) - 1;
-                    u64 g = 0;
-                    if (lane == l2) {
-                        g = atomicAdd(cand_count, (u64)cs);
-                        if (g <= cap && g + cs > cap) atomicAdd(&acc[C_OVF], 1ull);
-                    }
-                    g = __shfl(g, l2, WAVE);
-                    if (spill && g + rs < cap) cand_out[g + rs] = u;
-                }
-            }
-        });
-    // counts: wave reduce -> LDS -> one atomic per workgroup
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    uint32_t *const reg = region[wid];
+    uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
+    uint32_t wfill = 0;                      // wave-uniform
+    u64 winside = 0;                         // wave-uniform
+
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(a.keys);
+    const u64 n = a.n_local;
+    u64 head = ((16u - (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u)) & 15u) >> 2;
+    if (head > n) head = n;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(p + head);
+    const u64 nv = (n - head) >> 2, tail0 = head + (nv << 2);
+    const u64 tile = (u64)BLK * U, nfull = nv / tile;
+    // full tiles: grid-strided, every load of a tile issued before any use
+    for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
+        const uint4 *src = v + t * tile + threadIdx.x;
+        uint4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
+        uint32_t kk[K];
+        uint32_t cm = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            kk[4 * u + 0] = x[u].x ^ 0x80000000u;
+            kk[4 * u + 1] = x[u].y ^ 0x80000000u;
+            kk[4 * u + 2] = x[u].z ^ 0x80000000u;
+            kk[4 * u + 3] = x[u].w ^ 0x80000000u;
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t key = kk[j];
+            clt += key < lo;
+            ceqlo += key == lo;
+            ceqhi += key == hi;
+            cm |= ((key > lo) & (key < hi)) ? (1u << j) : 0u;
+        }
+        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
+    }
+    // ragged end: the last partial tile, as one masked tile of one workgroup
+    const u64 rem0 = nfull * tile;
+    if (blockIdx.x == (uint32_t)(nfull % gridDim.x)) {
+        uint32_t kk[K];
+        uint32_t ok = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 i = rem0 + u * BLK + threadIdx.x;
+            const bool in = i < nv;
+            const uint4 x = in ? v[i] : make_uint4(0, 0, 0, 0);
+            kk[4 * u + 0] = x.x ^ 0x80000000u;
+            kk[4 * u + 1] = x.y ^ 0x80000000u;
+            kk[4 * u + 2] = x.z ^ 0x80000000u;
+            kk[4 * u + 3] = x.w ^ 0x80000000u;
+            ok |= in ? (0xFu << (4 * u)) : 0u;
+        }
+        uint32_t cm = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t key = kk[j];
+            const bool in = (ok >> j) & 1u;
+            clt += (in & (key < lo)) ? 1u : 0u;
+            ceqlo += (in & (key == lo)) ? 1u : 0u;
+            ceqhi += (in & (key == hi)) ? 1u : 0u;
+            cm |= (in & (key > lo) & (key < hi)) ? (1u << j) : 0u;
+        }
+        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
+    }
+    if (blockIdx.x == 0) {  // the < 4-key unaligned head and tail
+        uint32_t kk[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) kk[j] = 0;
+        const bool okh = threadIdx.x < head, okt = threadIdx.x < n - tail0;
+        kk[0] = (okh ? p[threadIdx.x] : 0u) ^ 0x80000000u;
+        kk[1] = (okt ? p[tail0 + threadIdx.x] : 0u) ^ 0x80000000u;
+        const uint32_t ok = (okh ? 1u : 0u) | (okt ? 2u : 0u);
+        uint32_t cm = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t key = kk[j];
+            const bool in = (ok >> j) & 1u;
+            clt += (in & (key < lo)) ? 1u : 0u;
+            ceqlo += (in & (key == lo)) ? 1u : 0u;
+            ceqhi += (in & (key == hi)) ? 1u : 0u;
+            cm |= (in & (key > lo) & (key < hi)) ? (1u << j) : 0u;
+        }
+        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
+    }
+    if (wfill) {  // final flush of this wave's region
+        __builtin_amdgcn_wave_barrier();
+        const u64 g = reserve_cands(cand_count, acc, cap, wfill);
+        for (uint32_t i = lane; i < wfill; i += WAVE)
+            if (g + i < cap) cand_out[g + i] = reg[i];
+    }
+    // counts: wave reduce -> LDS -> one atomic per workgroup and counter
     u64 r0 = clt, r1 = ceqlo, r2 = ceqhi;
 #pragma unroll
     for (int o = WAVE / 2; o > 0; o >>= 1) {
@@ -402,37 +571,19 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         r1 += __shfl_xor(r1, o, WAVE);
         r2 += __shfl_xor(r2, o, WAVE);
     }
-    const int wid = threadIdx.x / WAVE;
     if (lane == 0) {
         red[0][wid] = r0;
         red[1][wid] = r1;
         red[2][wid] = r2;
+        red[3][wid] = winside;
     }
     __syncthreads();
-    const uint32_t total = lcount;
-    const uint32_t nl = total < (uint32_t)LBUF ? total : (uint32_t)LBUF;
-    if (threadIdx.x == 0) {
-        u64 s0 = 0, s1 = 0, s2 = 0;
-        for (int w = 0; w < BLK / WAVE; ++w) {
-            s0 += red[0][w];
-            s1 += red[1][w];
-            s2 += red[2][w];
-        }
-        if (s0) atomicAdd(&acc[C_LT], s0);
-        if (s1) atomicAdd(&acc[C_EQLO], s1);
-        if (s2) atomicAdd(&acc[C_EQHI], s2);
-        if (total) atomicAdd(&acc[C_IN], (u64)total);
-        u64 g = 0;
-        if (nl) {
-            g = atomicAdd(cand_count, (u64)nl);
-            if (g <= cap && g + nl > cap) atomicAdd(&acc[C_OVF], 1ull);
-        }
-        gbase = g;
+    if (threadIdx.x < 4) {
+        u64 sum = 0;
+        for (int w = 0; w < BLK / WAVE; ++w) sum += red[threadIdx.x][w];
+        const int slot[4] = {C_LT, C_EQLO, C_EQHI, C_IN};
+        if (sum) atomicAdd(&acc[slot[threadIdx.x]], sum);
     }
-    __syncthreads();
-    const u64 g = gbase;
-    for (uint32_t i = threadIdx.x; i < nl; i += BLK)
-        if (g + i < cap) cand_out[g + i] = lbuf[i];
 }
 
 // Final digit: one workgroup.  Writes the answer and the error word, then

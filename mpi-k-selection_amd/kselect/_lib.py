@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.environ.get("KTH_LIB", os.path.join(PKG_ROOT, "lib", "libkth.so"))
+LIB_PATH = os.environ.get("KTH_LIB") or os.path.join(PKG_ROOT, "lib", "libkth.so")
 
 KTH_OK = 0
 KTH_EINVAL = -1

@@ -185,7 +185,7 @@ def shipped():
             true = int(np.partition(a, k - 1)[k - 1])
             for P in (2, 8):
                 env = dict(os.environ, KO_TIME="1", KO_INPUT=path)
-                val, _ = run_cgm(os.path.join(REF_DIR, prog), P, env, 120)
+                val, _ = run_cgm(os.path.join(REF_DIR, prog), P, env, 60)
                 rec = {"program": prog, "P": P, "family": fam, "seed": G.DEFAULT_SEED, "n": n, "k": k,
                        "printed": val, "true": true}
                 print(rec, flush=True)
