@@ -114,7 +114,9 @@ def _vec_ops(L, seed):
         elif op == 6:
             trace.append(("search", L.VecSearch(v, i, x)))
         else:
-            trace.append(("stat", L.VecGetSize(v), L.VecIsFull(v), L.MinFind(v), L.AverageFind(v)))
+            n = L.VecGetSize(v)
+            # MinFind of an empty vector reads uninitialised data[0] in the reference
+            trace.append(("stat", n, L.VecIsFull(v), L.MinFind(v) if n else None, L.AverageFind(v)))
     n = L.VecGetSize(v)
     trace.append(("final", [L.VecGet(v, j) for j in range(n)]))
     L.VecDelete(v)
