@@ -151,6 +151,9 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    # one explicit stream for everything (torch ops, the selector, RCCL): the
+    # legacy null stream would add implicit synchronisation to every launch
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

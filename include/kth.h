@@ -17,8 +17,10 @@
  *   - Return value is 0 (KTH_OK) or a negative KTH_E* code; the answer goes to
  *     *out, never in-band (the in-band VecGet sentinels live in vector.h's
  *     VecKthSelect only).
- *   - Streams are passed as `void *` holding a hipStream_t (NULL = the ctx's own
- *     stream).  No C++ or framework types cross this boundary.
+ *   - Streams are passed as `void *` holding a hipStream_t (NULL = HIP's null
+ *     stream).  A new ctx owns a private non-blocking stream until
+ *     kth_ctx_set_stream replaces it.  No C++ or framework types cross this
+ *     boundary.
  *   - A kth_ctx is not thread-safe: one ctx per host thread or device.
  *   - The product path has no CPU fallback: without a usable GPU every compute
  *     entry point returns KTH_ENODEV.

@@ -34,6 +34,7 @@ int gather_grid(u64 nchunks) {
     return (int)std::max<u64>(1, (nchunks + per_wg - 1) / per_wg);
 }
 constexpr size_t ISLOT_WORDS = 3 * (size_t)kth::STATS_WORDS + 2;  // 3 slots + cand_count + pad
+static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
 
 #define HIP_TRY(x)                                                                                    \
@@ -76,6 +77,9 @@ struct kth_ctx {
     std::vector<hipEvent_t> ev_main, ev_total;
     int main_used = 0, total_used = 0;
     bool dirty = false;  // a launch sequence was cut short: re-zero the slots
+    // KTH_STAMPS=1 diagnostics: per-launch [WG][8] wall-clock stamps, dumped after each select
+    u64 *stamps = nullptr;
+    int stamp_next = 0;
     // sharded protocol
     u64 *uslots = nullptr;
     int64_t dist_n = 0, dist_k = 0, dist_cap = 0;
@@ -129,9 +133,70 @@ void window_ranks(int64_t n, int64_t k, int64_t s, u64 *r_lo, u64 *r_hi) {
     *r_hi = hi > (double)s ? (u64)s + 1 : (u64)std::max(1.0, hi);  // s+1 = no upper bound
 }
 
+constexpr int STAMP_LAUNCHES = 16, STAMP_WGS = 4096;
+u64 *next_stamps(kth_ctx *c) {
+    if (!c->stamps || c->stamp_next >= STAMP_LAUNCHES) return nullptr;
+    return c->stamps + (size_t)(c->stamp_next++) * STAMP_WGS * 8;
+}
+
+// Per launch of the last select: WGs, and mean / max of each stamp relative to
+// the launch's first entry, then the gap to the next launch (microseconds).
+void dump_stamps(kth_ctx *c) {
+    if (!c->stamps) return;
+    std::vector<u64> h((size_t)STAMP_LAUNCHES * STAMP_WGS * 8);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipMemcpy(h.data(), c->stamps, h.size() * 8, hipMemcpyDeviceToHost);
+    u64 prev_end = 0;
+    for (int l = 0; l < c->stamp_next; ++l) {
+        const u64 *b = h.data() + (size_t)l * STAMP_WGS * 8;
+        u64 t0 = ~0ull, tend = 0;
+        int nwg = 0;
+        for (int w = 0; w < STAMP_WGS; ++w)
+            if (b[w * 8]) {
+                nwg++;
+                t0 = std::min(t0, b[w * 8]);
+                for (int i = 0; i < 8; ++i) tend = std::max(tend, b[w * 8 + i]);
+            }
+        if (!nwg) continue;
+        fprintf(stderr, "kth-stamps launch %d wgs %4d gap %7.2f |", l, nwg, prev_end ? (t0 - prev_end) / 100.0 : 0.0);
+        for (int i = 0; i < 8; ++i) {
+            double sum = 0, mx = 0;
+            int cnt = 0;
+            for (int w = 0; w < STAMP_WGS; ++w)
+                if (b[w * 8] && b[w * 8 + i]) {
+                    const double d = (b[w * 8 + i] - t0) / 100.0;
+                    sum += d;
+                    mx = std::max(mx, d);
+                    cnt++;
+                }
+            if (cnt) fprintf(stderr, " p%d %6.2f/%6.2f", i, sum / cnt, mx);
+        }
+        fprintf(stderr, "\n");
+        if (nwg >= 512) {  // streaming pass: finish times (p3) by blockIdx % 8 (XCD under round-robin dispatch)
+            for (int x = 0; x < 8; ++x) {
+                double sum = 0, mn = 1e30, mx = 0;
+                int cnt = 0;
+                for (int w = x; w < STAMP_WGS; w += 8)
+                    if (b[w * 8] && b[w * 8 + 3]) {
+                        const double d = (b[w * 8 + 3] - t0) / 100.0;
+                        sum += d;
+                        mn = std::min(mn, d);
+                        mx = std::max(mx, d);
+                        cnt++;
+                    }
+                if (cnt) fprintf(stderr, "kth-stamps   wg%%8=%d p3 min %7.2f mean %7.2f max %7.2f\n", x, mn, sum / cnt, mx);
+            }
+        }
+        prev_end = tend;
+    }
+    (void)hipMemsetAsync(c->stamps, 0, h.size() * 8, c->stream);
+    c->stamp_next = 0;
+}
+
 StepArgs step(kth_ctx *c, int adv, int st_in, int st_out, const u64 *in, u64 *acc, u64 *zero) {
     StepArgs a;
     memset(&a, 0, sizeof a);
+    a.stamps = next_stamps(c);
     a.st_in = st_in >= 0 ? c->st + st_in : nullptr;
     a.st_out = c->st + st_out;
     a.stats_in = in;
@@ -281,13 +346,16 @@ int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_
         c->dirty = false;
     }
     int rc;
+    ev_mark(c, c->ev_total, c->total_used);
     if (n <= SMALL_N)
         rc = run_small(c, d_keys, n, k, d_out, d_status);
     else if (n <= RADIX_MAX_N)
         rc = run_radix(c, d_keys, n, k, d_out, d_status);
     else
         rc = run_window(c, d_keys, n, k, d_out, d_status);
+    ev_mark(c, c->ev_total, c->total_used);
     if (rc != KTH_OK) c->dirty = true;
+    if (c->stamps) dump_stamps(c);
     return rc;
 }
 
@@ -339,6 +407,13 @@ int kth_ctx_create(int device, kth_ctx **out) {
     if (device < 0 || device >= ndev) return KTH_EINVAL;
     kth_ctx *c = new kth_ctx();
     c->device = device;
+    if (getenv("KTH_STAMPS")) {
+        const size_t bytes = (size_t)STAMP_LAUNCHES * STAMP_WGS * 8 * 8;
+        if (hipMalloc(reinterpret_cast<void **>(&c->stamps), bytes) != hipSuccess || hipMemset(c->stamps, 0, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            c->stamps = nullptr;
+        }
+    }
     int rc = KTH_OK;
     do {
         if (hipSetDevice(device) != hipSuccess) { rc = KTH_EHIP; break; }
@@ -363,7 +438,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             }
             (void)hipGetLastError();
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
-            if (e) per = std::max(1, atoi(e));
+            if (e && atoi(e) > 0) per = atoi(e);
             c->main_grid = c->num_cu * per;
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
@@ -410,6 +485,7 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->cand) (void)hipFree(c->cand);
     if (c->staging) (void)hipFree(c->staging);
     if (c->d_status) (void)hipFree(c->d_status);
+    if (c->stamps) (void)hipFree(c->stamps);
     if (c->h_status) (void)hipHostFree(c->h_status);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -425,14 +501,11 @@ int kth_ctx_set_stream(kth_ctx *c, void *s) {
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamDestroy(c->stream);
         c->own_stream = false;
-        c->stream = nullptr;
     }
-    if (s) {
-        c->stream = reinterpret_cast<hipStream_t>(s);
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        c->own_stream = true;
-    }
+    // NULL is HIP's null stream (what torch calls the default stream): it
+    // orders against every blocking stream of the device, as a caller that
+    // passes its "current stream" expects.
+    c->stream = reinterpret_cast<hipStream_t>(s);
     return KTH_OK;
 }
 

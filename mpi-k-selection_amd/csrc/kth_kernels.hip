@@ -56,7 +56,16 @@ struct StepArgs {
     int adv;
     u64 init_n, init_k, init_s, r_lo, r_hi;
     u64 min_per_wg;        // keys per active workgroup (sets how many WGs flush a histogram)
+    u64 *stamps;           // KTH_STAMPS diagnostics: [gridDim.x][8] wall-clock stamps, else null
 };
+
+// Diagnostic phase stamps (KTH_STAMPS=1 only; null pointer in the product):
+// thread 0 of each workgroup records the 100 MHz wall clock at point i.
+#define KTH_STAMP(a, i)                                                                          \
+    do {                                                                                         \
+        if ((a).stamps && threadIdx.x == 0)                                                      \
+            (a).stamps[(u64)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();           \
+    } while (0)
 
 // ------------------------------------------------------------- the advance
 __device__ __forceinline__ void resolve(SelState &s) {
@@ -314,7 +323,9 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     __shared__ SelState ss;
     __shared__ u64 scratch[BLOCK / WAVE + 4];
     __shared__ uint32_t lh[2][NBINS];
+    KTH_STAMP(a, 0);
     advance<BLOCK>(ss, a, scratch);
+    KTH_STAMP(a, 1);
     bool share;
     const HistPlan plan = make_plan(ss, &share);
     const uint32_t mode = ss.mode;
@@ -333,6 +344,7 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     if (blockIdx.x >= active) return;
     for (int i = threadIdx.x; i < 2 * NBINS; i += BLOCK) (&lh[0][0])[i] = 0;
     __syncthreads();
+    KTH_STAMP(a, 2);
     auto f = [&](const uint32_t *k, uint32_t valid, auto full) {
 #pragma unroll
         for (int j = 0; j < 4 * LEVEL_UNROLL; ++j)
@@ -344,7 +356,9 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     else
         stream_tiles<BLOCK, LEVEL_UNROLL, false>(mode == MODE_SAMPLE ? a.sample : a.cand, count, blockIdx.x, active,
                                                  f);
+    KTH_STAMP(a, 3);
     hist_flush<BLOCK>(lh, plan, a.stats_acc);
+    KTH_STAMP(a, 5);
 }
 
 // Sample gather: s keys in chunks of 64 contiguous keys spread evenly over the
@@ -358,6 +372,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
     __shared__ uint32_t lh[2][NBINS];
     HistPlan plan;
     bool share = false;
+    KTH_STAMP(a, 0);
     if (FUSE) {
         advance<DENSE_BLK>(ss, a, scratch);
         plan = make_plan(ss, &share);
@@ -386,7 +401,9 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
             }
         }
     }
+    KTH_STAMP(a, 3);
     if (FUSE) hist_flush<DENSE_BLK>(lh, plan, a.stats_acc);
+    KTH_STAMP(a, 5);
 }
 
 // The streaming pass.  Window [lo, hi] comes from the advance (last sample
@@ -464,8 +481,10 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     __shared__ u64 scratch[BLK / WAVE + 4];
     __shared__ uint32_t region[BLK / WAVE][WREG];
     __shared__ u64 red[4][BLK / WAVE];
+    KTH_STAMP(a, 0);
     advance<BLK>(ss, a, scratch);
     publish<BLK>(ss, 0, a);
+    KTH_STAMP(a, 1);
     if (ss.mode != MODE_MAIN) return;  // block-uniform (error or resolved)
     const uint32_t lo = ss.lo, hi = ss.hi;
     const u64 cap = a.cap;
@@ -584,6 +603,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         const int slot[4] = {C_LT, C_EQLO, C_EQHI, C_IN};
         if (sum) atomicAdd(&acc[slot[threadIdx.x]], sum);
     }
+    KTH_STAMP(a, 5);
 }
 
 // Final digit: one workgroup.  Writes the answer and the error word, then
@@ -592,6 +612,7 @@ __global__ __launch_bounds__(BLK) void k_result(StepArgs a, int32_t *d_out, int3
                                                 u64 izero_words) {
     __shared__ SelState ss;
     __shared__ u64 scratch[BLK / WAVE + 4];
+    KTH_STAMP(a, 0);
     advance<BLK>(ss, a, scratch);
     if (threadIdx.x == 0) {
         SelState o = ss;
@@ -605,6 +626,7 @@ __global__ __launch_bounds__(BLK) void k_result(StepArgs a, int32_t *d_out, int3
     }
     __syncthreads();
     for (u64 i = threadIdx.x; i < izero_words; i += BLK) izero[i] = 0;
+    KTH_STAMP(a, 5);
 }
 
 // n <= 16384: whole selection in one workgroup, keys in LDS.

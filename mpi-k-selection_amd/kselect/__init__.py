@@ -75,11 +75,12 @@ def _ptr(x):
 
 
 def _stream_handle(stream):
+    """hipStream_t of a torch stream (0 / None = the null stream, torch's default)."""
     if stream is None:
         return None
     if isinstance(stream, int):
-        return stream
-    return stream.cuda_stream  # torch.cuda.Stream
+        return stream or None
+    return stream.cuda_stream or None  # torch.cuda.Stream
 
 
 class Selector:
