@@ -57,6 +57,7 @@ constexpr int MAX_EVENTS = 4 * 2048;
 struct kth_ctx {
     int device = 0;
     int main_grid = 0;  // streaming-pass workgroups (num_cu * 8; KTH_MAIN_WG_PER_CU overrides)
+    u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -238,12 +239,14 @@ int level_grid(u64 count, u64 per_wg) {
     return (int)std::max<u64>(1, std::min<u64>(LEVEL_GRID_MAX, g));
 }
 
+u64 sparse_wg(const kth_ctx *c) { return c->sparse_per_wg ? c->sparse_per_wg : SPARSE_PER_WG; }
+
 void launch_level(kth_ctx *c, StepArgs a, bool dense, int grid) {
     if (dense) {
         a.min_per_wg = DENSE_PER_WG;
         kth::k_level<kth::DENSE_BLK><<<grid, kth::DENSE_BLK, 0, c->stream>>>(a);
     } else {
-        a.min_per_wg = SPARSE_PER_WG;
+        a.min_per_wg = sparse_wg(c);
         kth::k_level<kth::BLK><<<grid, kth::BLK, 0, c->stream>>>(a);
     }
 }
@@ -270,11 +273,11 @@ int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.keys = keys;
     a.n_local = (u64)n;
-    launch_level(c, a, false, level_grid((u64)n, SPARSE_PER_WG));
+    launch_level(c, a, false, level_grid((u64)n, sparse_wg(c)));
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 2), islot(c, 0), islot(c, 1));
     a.keys = keys;
     a.n_local = (u64)n;
-    launch_level(c, a, false, level_grid((u64)n, SPARSE_PER_WG));
+    launch_level(c, a, false, level_grid((u64)n, sparse_wg(c)));
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), nullptr, nullptr);
     kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
     c->last_state = 1;
@@ -302,7 +305,7 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.r_hi = r_hi;
     kth::k_gather<true><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, keys, stride, c->sample, (u64)s);
     // digits 2, 3 of the sample ranks (sparse: only keys in the picked bins)
-    const int gs = level_grid((u64)s, SPARSE_PER_WG);
+    const int gs = level_grid((u64)s, sparse_wg(c));
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.sample = c->sample;
     a.sample_count = (u64)s;
@@ -439,6 +442,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             (void)hipGetLastError();
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
             if (e && atoi(e) > 0) per = atoi(e);
+            if (const char *g = getenv("KTH_SPARSE_PER_WG")) c->sparse_per_wg = (u64)std::max(0, atoi(g));
             c->main_grid = c->num_cu * per;
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
@@ -706,7 +710,7 @@ int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
     a.sample = d_sample;
     a.sample_count = (u64)s_total;
     launch_level(c, a, true, level_grid((u64)s_total, DENSE_PER_WG));
-    const int gs = level_grid((u64)s_total, SPARSE_PER_WG);
+    const int gs = level_grid((u64)s_total, sparse_wg(c));
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
     a.sample = d_sample;
     a.sample_count = (u64)s_total;

@@ -28,6 +28,8 @@ import torch.distributed as dist
 
 from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check
 
+SMALL_PER_RANK = 64  # below this many keys per rank: all-gather and select locally
+
 
 def shard_bounds(n, rank, world):
     """Block partition of TODO-kth-problem-cgm.c:81-100: sizev[i] = n/P + (i < n%P)."""
@@ -82,6 +84,10 @@ class HipBackend:
     def alloc_out(self):
         return torch.empty(1, dtype=torch.int32, device=self.device)
 
+    def select_all(self, keys, n, k, out):
+        """k-th smallest of keys[0..n) on this GPU (the small-input path)."""
+        self.sel.select_async(keys, n, k, out)
+
 
 class DistSelector:
     """k-th smallest of the union of every rank's shard (global 1-based k)."""
@@ -99,11 +105,19 @@ class DistSelector:
         """Enqueue one selection; returns the device (or CPU, for gloo) int32[1] answer tensor.
 
         n_total must be the sum of n_local over ranks and k in [1, n_total];
-        every rank must pass the same (n_total, k)."""
+        every rank must pass the same (n_total, k).  Shards are expected to be
+        balanced (every n_local >= n_total // world, as the block partition of
+        shard_bounds gives); below SMALL_PER_RANK keys per rank the shards are
+        all-gathered and every rank selects from the union."""
         if not (1 <= k <= n_total):
             raise ValueError(f"k={k} outside [1, {n_total}]")
         b = self.b
+        if n_total // self.world < SMALL_PER_RANK:
+            return self._select_small(shard, n_local, n_total, k)
         s_local = b.sample_size(n_total // self.world)
+        if n_local < s_local:
+            raise ValueError(f"shard of {n_local} keys is smaller than the per-rank sample ({s_local}); "
+                             "use balanced shards (kselect.dist.shard_bounds)")
         if self._sample is None or self._sample.numel() != s_local:
             self._sample = b.alloc_sample(s_local)
             self._gathered = b.alloc_sample(s_local * self.world)
@@ -117,4 +131,21 @@ class DistSelector:
             i = b.level(shard, n_local, level)
             dist.all_reduce(self.slots[i], op=dist.ReduceOp.SUM, group=self.group)
         b.result(self.out)
+        return self.out
+
+    def _select_small(self, shard, n_local, n_total, k):
+        """Tiny inputs (cf. the reference's final Gatherv + solve on one rank,
+        TODO-kth-problem-cgm.c:235-278): all-gather the shards, select locally."""
+        sizes = [torch.zeros(1, dtype=torch.int64, device=self.out.device) for _ in range(self.world)]
+        dist.all_gather(sizes, torch.tensor([n_local], dtype=torch.int64, device=self.out.device), group=self.group)
+        sizes = [int(x.item()) for x in sizes]
+        if sum(sizes) != n_total:
+            raise ValueError(f"shard sizes {sizes} do not sum to n_total={n_total}")
+        m = max(sizes)
+        padded = torch.zeros(m, dtype=torch.int32, device=self.out.device)
+        padded[:n_local] = shard[:n_local]
+        gathered = torch.empty(m * self.world, dtype=torch.int32, device=self.out.device)
+        dist.all_gather_into_tensor(gathered, padded, group=self.group)
+        union = torch.cat([gathered[r * m:r * m + sizes[r]] for r in range(self.world)])
+        self.b.select_all(union, n_total, k, self.out)
         return self.out

@@ -56,6 +56,9 @@ class CpuBackend:
     def alloc_out(self):
         return torch.empty(1, dtype=torch.int32)
 
+    def select_all(self, keys, n, k, out):
+        out[0] = int(np.sort(keys.numpy()[:n])[k - 1])
+
     # -- steps --------------------------------------------------------------
     def begin(self, slots, n_total, k):
         self.slots = slots

@@ -47,7 +47,8 @@ def _worker(rank, world, port, cases, q):
             shard = torch.from_numpy(G.gen(cnt, G.BY_NAME[fam], 0x5EED0001, param, offset=start, n_total=n))
             for k in ks:
                 got = int(ds.select(shard, cnt, n, k)[0])
-                out.append((fam, n, k, got, ds.b.path))
+                out.append((fam, n, k, got, getattr(ds.b, "path", "small")))
+                ds.b.path = "small"  # reset: the next select sets it again unless it takes the small path
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -73,6 +74,8 @@ def _expected(fam, param, n):
 
 
 CASES = [
+    ("uniform_full", 0, 7, None, None),      # fewer keys than ranks on some ranks: all-gather path
+    ("few_distinct", 0, 100, None, None),
     ("uniform_full", 0, 600_001, None, None),
     ("uniform_half", 0, 400_000, None, None),
     ("few_distinct", 0, 300_000, None, None),
@@ -86,7 +89,7 @@ CASES = [
 def test_dist_selector_gloo(world):
     cases = []
     for fam, param, n, _, cap in CASES:
-        ks = [1, 2, n // 3, n // 2, n - 1, n]
+        ks = sorted({k for k in (1, 2, n // 3, n // 2, n - 1, n) if 1 <= k <= n})
         cases.append((fam, param, n, ks, cap))
     res = _run(world, cases)
     by_rank = [res[r] for r in range(world)]
