@@ -374,6 +374,39 @@ bool is_device_ptr(const void *p) {
 
 thread_local kth_ctx *tl_ctx = nullptr;
 
+// Rows: the wave-per-row register kernel (kth_rows.hpp) for cols <= 4096,
+// KPL keys per lane; the LDS workgroup-per-row kernel above that.
+#ifndef KTH_ROWS_R0
+#define KTH_ROWS_R0 4  // first-pass histogram copies per wave in k_rows_reg
+#endif
+template <bool F32, int KPL>
+void launch_rows_reg(kth_ctx *c, bool vec, int g, const uint32_t *d_keys, u64 R, uint32_t C, uint32_t K,
+                     uint32_t *d_out) {
+    if (vec)
+        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0><<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out);
+    else
+        kth::k_rows_reg<F32, KPL, false, KTH_ROWS_R0><<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out);
+}
+
+template <bool F32>
+int launch_rows(kth_ctx *c, const uint32_t *d_keys, int64_t rows, int32_t cols, int32_t k, uint32_t *d_out) {
+    const bool vec = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0 && cols % 4 == 0;
+    const int rows_per_wg = kth::RW_BLOCK / kth::WAVE;
+    const int g = (int)std::min<int64_t>((rows + rows_per_wg - 1) / rows_per_wg, (int64_t)c->num_cu * 64);
+    const u64 R = (u64)rows;
+    const uint32_t C = (uint32_t)cols, K = (uint32_t)k;
+    if (cols <= 1024)
+        launch_rows_reg<F32, 16>(c, vec, g, d_keys, R, C, K, d_out);
+    else if (cols <= 2048)
+        launch_rows_reg<F32, 32>(c, vec, g, d_keys, R, C, K, d_out);
+    else if (cols <= 4096)
+        launch_rows_reg<F32, 64>(c, vec, g, d_keys, R, C, K, d_out);
+    else
+        kth::k_rows<F32><<<(int)std::min<int64_t>(rows, 1 << 20), kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
+            d_keys, R, C, (u64)k, d_out);
+    return launch_check();
+}
+
 }  // namespace
 
 // ====================================================================== API
@@ -634,11 +667,8 @@ int kth_select_rows_i32(kth_ctx *c, const int32_t *d_keys, int64_t rows, int32_t
         return KTH_EINVAL;
     if (rows == 0) return KTH_OK;
     KTH_TRY(set_device(c));
-    const int g = (int)std::min<int64_t>(rows, 1 << 20);
-    kth::k_rows<false><<<g, kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
-        reinterpret_cast<const uint32_t *>(d_keys), (u64)rows, (uint32_t)cols, (u64)k,
-        reinterpret_cast<uint32_t *>(d_out));
-    return launch_check();
+    return launch_rows<false>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
+                              reinterpret_cast<uint32_t *>(d_out));
 }
 
 int kth_select_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t cols, int32_t k, float *d_out) {
@@ -646,11 +676,8 @@ int kth_select_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t c
         return KTH_EINVAL;
     if (rows == 0) return KTH_OK;
     KTH_TRY(set_device(c));
-    const int g = (int)std::min<int64_t>(rows, 1 << 20);
-    kth::k_rows<true><<<g, kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
-        reinterpret_cast<const uint32_t *>(d_keys), (u64)rows, (uint32_t)cols, (u64)k,
-        reinterpret_cast<uint32_t *>(d_out));
-    return launch_check();
+    return launch_rows<true>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
+                             reinterpret_cast<uint32_t *>(d_out));
 }
 
 int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, int64_t n_total, int dist, uint64_t seed,

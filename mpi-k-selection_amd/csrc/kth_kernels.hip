@@ -769,3 +769,5 @@ __global__ __launch_bounds__(BLK) void k_fill(int32_t *__restrict__ out, u64 n, 
 }
 
 }  // namespace kth
+
+#include "kth_rows.hpp"

@@ -191,7 +191,7 @@ def _row_ref(m, k):
     return np.sort(m, axis=1, kind="stable")[:, k - 1]
 
 
-@pytest.mark.parametrize("cols", [1, 7, 4096, 5000, 16384])
+@pytest.mark.parametrize("cols", [1, 7, 1000, 1024, 1500, 2048, 4093, 4096, 5000, 16384])
 def test_rows_i32(gpu, cols):
     import torch
     rows = 257
@@ -206,6 +206,26 @@ def test_rows_i32(gpu, cols):
         np.testing.assert_array_equal(out.cpu().numpy(), _row_ref(m, k), err_msg=f"k={k}")
 
 
+def test_rows_unaligned_and_adversarial(gpu):
+    """Wave-per-row kernel: a base pointer 4 bytes off 16-byte alignment (scalar
+    load path), all-equal rows at INT_MIN / INT_MAX, and rows of two values."""
+    import torch
+    rows, cols = 300, 4096
+    rng = np.random.default_rng(11)
+    m = rng.integers(-2 ** 31, 2 ** 31, size=(rows, cols + 1), dtype=np.int64).astype(np.int32)
+    m[0] = -2 ** 31
+    m[1] = 2 ** 31 - 1
+    m[2] = rng.choice(np.array([5, -5], dtype=np.int32), size=cols + 1)
+    flat = torch.from_numpy(m.reshape(-1)).cuda()
+    sub = flat[1:1 + rows * cols]  # 4-byte aligned, not 16
+    host = sub.cpu().numpy().reshape(rows, cols)
+    out = torch.empty(rows, dtype=torch.int32, device="cuda")
+    for k in (1, 2, 64, cols // 2, cols - 1, cols):
+        gpu.rows(sub, rows, cols, k, out)
+        gpu.sync()
+        np.testing.assert_array_equal(out.cpu().numpy(), _row_ref(host, k), err_msg=f"k={k}")
+
+
 def _f32_order_key(x):
     b = x.view(np.uint32).astype(np.uint64)
     nan = np.isnan(x)
@@ -213,7 +233,7 @@ def _f32_order_key(x):
     return np.where(nan, 0xFFFFFFFF, key)
 
 
-@pytest.mark.parametrize("cols", [4096, 333])
+@pytest.mark.parametrize("cols", [4096, 2048, 333, 6000])
 def test_rows_f32(gpu, cols):
     import torch
     rows = 129
