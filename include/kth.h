@@ -115,6 +115,19 @@ int kth_select_rows_i32(kth_ctx *ctx, const int32_t *d_keys, int64_t rows, int32
 int kth_select_rows_f32(kth_ctx *ctx, const float *d_keys, int64_t rows, int32_t cols, int32_t k,
                         float *d_out);
 
+/* --- top-k per row (the MoE-routing shape) ---------------
+ * The k smallest keys of each row (largest != 0: the k largest), with their
+ * column indices, in column order; of the keys equal to the k-th, the first
+ * ones by column.  d_vals: rows x k values, d_idx: rows x k int32 columns;
+ * either may be NULL (not both).  1 <= k <= cols <= KTH_TOPK_MAX_COLS.  Same
+ * orders as kth_select_rows_* (float: IEEE total order, NaN above +inf, so
+ * NaNs come last for smallest and first for largest). */
+#define KTH_TOPK_MAX_COLS 4096
+int kth_topk_rows_i32(kth_ctx *ctx, const int32_t *d_keys, int64_t rows, int32_t cols, int32_t k, int largest,
+                      int32_t *d_vals, int32_t *d_idx);
+int kth_topk_rows_f32(kth_ctx *ctx, const float *d_keys, int64_t rows, int32_t cols, int32_t k, int largest,
+                      float *d_vals, int32_t *d_idx);
+
 /* --- synthetic inputs (bench / tests) --------------------------------------
  * Fills d_out[0..n) with the keys of global indices offset..offset+n of an
  * n_total-key input of family `dist` (oracle/kth_oracle.h enum ko_dist;

@@ -379,29 +379,34 @@ thread_local kth_ctx *tl_ctx = nullptr;
 #ifndef KTH_ROWS_R0
 #define KTH_ROWS_R0 4  // first-pass histogram copies per wave in k_rows_reg
 #endif
-template <bool F32, int KPL>
+template <bool F32, int KPL, bool TOPK>
 void launch_rows_reg(kth_ctx *c, bool vec, int g, const uint32_t *d_keys, u64 R, uint32_t C, uint32_t K,
-                     uint32_t *d_out) {
+                     uint32_t *d_out, uint32_t flip, uint32_t *vals, int32_t *idx) {
     if (vec)
-        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0><<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out);
+        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0, TOPK>
+            <<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out, flip, vals, idx);
     else
-        kth::k_rows_reg<F32, KPL, false, KTH_ROWS_R0><<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out);
+        kth::k_rows_reg<F32, KPL, false, KTH_ROWS_R0, TOPK>
+            <<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out, flip, vals, idx);
 }
 
-template <bool F32>
-int launch_rows(kth_ctx *c, const uint32_t *d_keys, int64_t rows, int32_t cols, int32_t k, uint32_t *d_out) {
+// k-th per row (TOPK = false, into d_out) or top-k per row (into vals / idx;
+// cols <= KTH_TOPK_MAX_COLS, checked by the caller).
+template <bool F32, bool TOPK>
+int launch_rows(kth_ctx *c, const uint32_t *d_keys, int64_t rows, int32_t cols, int32_t k, uint32_t *d_out,
+                uint32_t flip = 0, uint32_t *vals = nullptr, int32_t *idx = nullptr) {
     const bool vec = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0 && cols % 4 == 0;
     const int rows_per_wg = kth::RW_BLOCK / kth::WAVE;
     const int g = (int)std::min<int64_t>((rows + rows_per_wg - 1) / rows_per_wg, (int64_t)c->num_cu * 64);
     const u64 R = (u64)rows;
     const uint32_t C = (uint32_t)cols, K = (uint32_t)k;
     if (cols <= 1024)
-        launch_rows_reg<F32, 16>(c, vec, g, d_keys, R, C, K, d_out);
+        launch_rows_reg<F32, 16, TOPK>(c, vec, g, d_keys, R, C, K, d_out, flip, vals, idx);
     else if (cols <= 2048)
-        launch_rows_reg<F32, 32>(c, vec, g, d_keys, R, C, K, d_out);
+        launch_rows_reg<F32, 32, TOPK>(c, vec, g, d_keys, R, C, K, d_out, flip, vals, idx);
     else if (cols <= 4096)
-        launch_rows_reg<F32, 64>(c, vec, g, d_keys, R, C, K, d_out);
-    else
+        launch_rows_reg<F32, 64, TOPK>(c, vec, g, d_keys, R, C, K, d_out, flip, vals, idx);
+    else if (!TOPK)
         kth::k_rows<F32><<<(int)std::min<int64_t>(rows, 1 << 20), kth::ROWS_BLOCK, (size_t)cols * 4, c->stream>>>(
             d_keys, R, C, (u64)k, d_out);
     return launch_check();
@@ -667,7 +672,7 @@ int kth_select_rows_i32(kth_ctx *c, const int32_t *d_keys, int64_t rows, int32_t
         return KTH_EINVAL;
     if (rows == 0) return KTH_OK;
     KTH_TRY(set_device(c));
-    return launch_rows<false>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
+    return launch_rows<false, false>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
                               reinterpret_cast<uint32_t *>(d_out));
 }
 
@@ -676,8 +681,30 @@ int kth_select_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t c
         return KTH_EINVAL;
     if (rows == 0) return KTH_OK;
     KTH_TRY(set_device(c));
-    return launch_rows<true>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
+    return launch_rows<true, false>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k,
                              reinterpret_cast<uint32_t *>(d_out));
+}
+
+int kth_topk_rows_i32(kth_ctx *c, const int32_t *d_keys, int64_t rows, int32_t cols, int32_t k, int largest,
+                      int32_t *d_vals, int32_t *d_idx) {
+    if (!c || !d_keys || (!d_vals && !d_idx) || rows < 0 || cols < 1 || cols > KTH_TOPK_MAX_COLS || k < 1 ||
+        k > cols)
+        return KTH_EINVAL;
+    if (rows == 0) return KTH_OK;
+    KTH_TRY(set_device(c));
+    return launch_rows<false, true>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k, nullptr,
+                                    largest ? 0xFFFFFFFFu : 0u, reinterpret_cast<uint32_t *>(d_vals), d_idx);
+}
+
+int kth_topk_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t cols, int32_t k, int largest,
+                      float *d_vals, int32_t *d_idx) {
+    if (!c || !d_keys || (!d_vals && !d_idx) || rows < 0 || cols < 1 || cols > KTH_TOPK_MAX_COLS || k < 1 ||
+        k > cols)
+        return KTH_EINVAL;
+    if (rows == 0) return KTH_OK;
+    KTH_TRY(set_device(c));
+    return launch_rows<true, true>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k, nullptr,
+                                   largest ? 0xFFFFFFFFu : 0u, reinterpret_cast<uint32_t *>(d_vals), d_idx);
 }
 
 int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, int64_t n_total, int dist, uint64_t seed,

@@ -24,9 +24,21 @@ constexpr int RW_BLOCK = 256;
 constexpr int RW_BINS = 256;
 constexpr int RW_STRIDE = RW_BINS + 1;  // words between histogram copies
 
-template <bool F32, int KPL, bool VEC, int R0>
+// Raw bits of a key (inverse of the order-preserving transform).
+template <bool F32>
+__device__ __forceinline__ uint32_t raw_of_key(uint32_t key) {
+    return F32 ? f32_of_key(key) : (uint32_t)i32_of_key(key);
+}
+
+// TOPK = false: out[r] = the k-th smallest of row r.
+// TOPK = true: vals[r*k ..] / idx[r*k ..] = the k smallest keys of row r and
+// their columns, in column order; of the keys equal to the k-th, the first
+// ones by column.  flip = 0xFFFFFFFF selects the k largest instead (the key
+// order reversed: ~key).
+template <bool F32, int KPL, bool VEC, int R0, bool TOPK>
 __global__ __launch_bounds__(RW_BLOCK) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
-                                                      uint32_t k, uint32_t *__restrict__ out) {
+                                                      uint32_t k, uint32_t *__restrict__ out, uint32_t flip,
+                                                      uint32_t *__restrict__ vals, int32_t *__restrict__ idx) {
     static_assert(KPL % 4 == 0, "16-byte loads");
     __shared__ uint32_t hist_all[RW_BLOCK / WAVE][R0 * RW_STRIDE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
@@ -50,7 +62,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_rows_reg(const uint32_t *__restric
             const uint32_t v[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                key[4 * j + q] = e + q < cols ? (F32 ? key_of_f32(v[q]) : key_of_i32(v[q])) : 0xFFFFFFFFu;
+                key[4 * j + q] = e + q < cols ? ((F32 ? key_of_f32(v[q]) : key_of_i32(v[q])) ^ flip) : 0xFFFFFFFFu;
         }
         uint32_t prefix = 0, kk = k, answer = 0;
         bool found = false;
@@ -118,7 +130,70 @@ __global__ __launch_bounds__(RW_BLOCK) void k_rows_reg(const uint32_t *__restric
             __builtin_amdgcn_wave_barrier();  // the next zeroing after every lane's histogram reads
         }
         if (!found) answer = prefix;
-        if (lane == 0) out[r] = F32 ? f32_of_key(answer) : (uint32_t)i32_of_key(answer);
+        if (!TOPK) {
+            if (lane == 0) out[r] = raw_of_key<F32>(answer ^ flip);
+        } else {
+            // Compaction in column order.  Group j holds columns (64*j + lane)*4 + q:
+            // lane-major, then q.  For each q a ballot of the selected keys and
+            // mbcnt (set bits in lower lanes) give every key its position: the
+            // keys selected before it = taken + sum_q mbcnt(ballot_q) + those of
+            // its own lane with a smaller q.  Ties: the keys equal to the k-th are
+            // ranked by column the same way, and the first kk of them are taken.
+            uint32_t taken = 0, eq_seen = 0;
+            const u64 obase = r * (u64)k;
+            const bool stage = 2 * k <= (uint32_t)(R0 * RW_STRIDE);  // fits the wave's histogram words
+            auto below_lane = [](unsigned long long b) {  // set bits of b in lanes below this one
+                return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            };
+#pragma unroll
+            for (int j = 0; j < KPL / 4; ++j) {
+                const uint32_t e = (uint32_t)(j * WAVE + lane) * 4u;
+                bool lt[4], eq[4], sel[4];
+                uint32_t eq_below = 0, eq_tot = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool valid = e + q < cols;
+                    lt[q] = valid && key[4 * j + q] < answer;
+                    eq[q] = valid && key[4 * j + q] == answer;
+                    const unsigned long long be = __ballot(eq[q]);
+                    eq_below += below_lane(be);
+                    eq_tot += (uint32_t)__popcll(be);
+                }
+                uint32_t rank = eq_seen + eq_below;  // tie rank of this lane's first equal key
+                uint32_t pos = taken, tot = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    sel[q] = lt[q] || (eq[q] && rank < kk);
+                    rank += eq[q] ? 1u : 0u;
+                    const unsigned long long bs = __ballot(sel[q]);
+                    pos += below_lane(bs);
+                    tot += (uint32_t)__popcll(bs);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (sel[q]) {
+                        const uint32_t x = raw_of_key<F32>(key[4 * j + q] ^ flip);
+                        if (stage) {  // the histogram is free now: stage (value, column) pairs
+                            hist[2 * pos] = x;
+                            hist[2 * pos + 1] = e + q;
+                        } else {
+                            if (vals) vals[obase + pos] = x;
+                            if (idx) idx[obase + pos] = (int32_t)(e + q);
+                        }
+                        ++pos;
+                    }
+                taken += tot;
+                eq_seen += eq_tot;
+                __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+            }
+            if (stage) {  // coalesced copy-out of the staged pairs
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t i = lane; i < k; i += WAVE) {
+                    if (vals) vals[obase + i] = hist[2 * i];
+                    if (idx) idx[obase + i] = (int32_t)hist[2 * i + 1];
+                }
+            }
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }

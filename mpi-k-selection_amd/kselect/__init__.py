@@ -33,6 +33,7 @@ from ._lib import (  # noqa: F401
     KTH_PATH_WINDOW_FALLBACK,
     KTH_ROWS_MAX_COLS,
     KTH_STATS_WORDS,
+    KTH_TOPK_MAX_COLS,
     IntVector,
     KthError,
     KthLibraryMissing,
@@ -149,6 +150,14 @@ class Selector:
     def rows(self, d_keys, rows, cols, k, d_out, f32=False):
         fn = LIB.kth_select_rows_f32 if f32 else LIB.kth_select_rows_i32
         check(fn(self._ctx, _ptr(d_keys), int(rows), int(cols), int(k), _ptr(d_out)), "kth_select_rows")
+
+    def topk_rows(self, d_keys, rows, cols, k, d_vals=None, d_idx=None, largest=False, f32=False):
+        """Per row: the k smallest (largest=True: largest) keys and their columns,
+        in column order, ties broken by column (kth_topk_rows_*)."""
+        fn = LIB.kth_topk_rows_f32 if f32 else LIB.kth_topk_rows_i32
+        check(fn(self._ctx, _ptr(d_keys), int(rows), int(cols), int(k), 1 if largest else 0,
+                 _ptr(d_vals) if d_vals is not None else None, _ptr(d_idx) if d_idx is not None else None),
+              "kth_topk_rows")
 
     def fill(self, d_out, n, family=UNIFORM_FULL, seed=DEFAULT_SEED, param=0, offset=0, n_total=None):
         if isinstance(family, str):

@@ -22,6 +22,7 @@ KTH_PATH_LDS, KTH_PATH_RADIX, KTH_PATH_WINDOW, KTH_PATH_WINDOW_FALLBACK = 1, 2, 
 KTH_STATS_WORDS = 8 + 2 * 2048
 KTH_DIST_LEVELS = 3
 KTH_ROWS_MAX_COLS = 16384
+KTH_TOPK_MAX_COLS = 4096
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -87,6 +88,10 @@ PROTOS = {
                                            ctypes.POINTER(ctypes.c_double)]),
     "kth_select_rows_i32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, c_vp]),
     "kth_select_rows_f32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, c_vp]),
+    "kth_topk_rows_i32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+                                         c_vp, c_vp]),
+    "kth_topk_rows_f32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
+                                         c_vp, c_vp]),
     "kth_fill_synthetic": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                           ctypes.c_uint64, ctypes.c_int32]),
     "kth_dist_begin": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64]),

@@ -255,6 +255,68 @@ def test_rows_f32(gpu, cols):
         np.testing.assert_array_equal(_f32_order_key(got), _f32_order_key(want), err_msg=f"k={k}")
 
 
+# ------------------------------------------------------------- top-k rows
+def _topk_ref(keys, k, largest):
+    """Column-order top-k with ties by column: numpy restatement of the contract
+    (include/kth.h kth_topk_rows_*), on order keys (u64 view of the total order)."""
+    order = -keys.astype(np.int64) if largest else keys.astype(np.int64)
+    rows, cols = keys.shape
+    idx = np.argsort(order, axis=1, kind="stable")[:, :k]  # stable: ties by column
+    return np.sort(idx, axis=1)  # column order
+
+
+def _i32_order_key(m):
+    return m.astype(np.int64)
+
+
+@pytest.mark.parametrize("cols,k", [(4096, 64), (4096, 1), (4096, 4096), (1500, 8), (7, 3), (2048, 2047)])
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_rows_i32(gpu, cols, k, largest):
+    import torch
+    rows = 193
+    rng = np.random.default_rng(cols * 7 + k)
+    m = rng.integers(-2 ** 31, 2 ** 31, size=(rows, cols), dtype=np.int64).astype(np.int32)
+    m[::4] = rng.integers(-3, 3, size=(len(m[::4]), cols))  # heavy ties
+    m[1] = 2 ** 31 - 1
+    d = torch.from_numpy(m).cuda()
+    vals = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+    idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+    gpu.topk_rows(d, rows, cols, k, vals, idx, largest=largest)
+    gpu.sync()
+    want_idx = _topk_ref(_i32_order_key(m), k, largest)
+    np.testing.assert_array_equal(idx.cpu().numpy(), want_idx)
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(m, want_idx, axis=1))
+
+
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_rows_f32(gpu, largest):
+    import torch
+    rows, cols, k = 129, 4096, 64
+    rng = np.random.default_rng(5)
+    m = rng.uniform(-1, 1, size=(rows, cols)).astype(np.float32)
+    m[1] = np.round(m[1] * 4) / 4
+    m[2, :6] = [np.nan, -0.0, 0.0, np.inf, -np.inf, np.nan]
+    d = torch.from_numpy(m).cuda()
+    vals = torch.empty((rows, k), dtype=torch.float32, device="cuda")
+    idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+    gpu.topk_rows(d, rows, cols, k, vals, idx, largest=largest, f32=True)
+    gpu.sync()
+    want_idx = _topk_ref(_f32_order_key(m).astype(np.int64), k, largest)
+    np.testing.assert_array_equal(idx.cpu().numpy(), want_idx)
+    got = vals.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, np.take_along_axis(m, want_idx, axis=1).view(np.uint32))
+
+
+def test_topk_rows_errors(gpu):
+    import kselect
+    import torch
+    d = torch.zeros((2, 5000), dtype=torch.int32, device="cuda")
+    out = torch.empty((2, 4), dtype=torch.int32, device="cuda")
+    for cols, k in ((5000, 4), (10, 0), (10, 11)):
+        with pytest.raises(kselect.KthError):
+            gpu.topk_rows(d, 2, cols, k, out, None)
+
+
 # ----------------------------------------------------- sharded, one rank
 def _free_port():
     s = socket.socket()
