@@ -169,8 +169,11 @@ int kth_dist_window(kth_ctx *ctx, const uint32_t *d_sample, int64_t s_total);
 int kth_dist_scan(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local);
 int kth_dist_level(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, int level);
 int kth_dist_result(kth_ctx *ctx, int32_t *d_out);
-/* Default sample size per rank for a shard of n_local keys. */
-int64_t kth_dist_sample_size(int64_t n_local);
+/* Sample size for n keys (the single-GPU rule: min(2^20, n/64), a multiple
+ * of 64).  Sharded callers take about kth_dist_sample_size(n_total) / P keys
+ * per rank (a multiple of 64, at least 64), so that the all-gathered sample
+ * has the single-GPU size. */
+int64_t kth_dist_sample_size(int64_t n);
 
 #ifdef __cplusplus
 }

@@ -236,7 +236,9 @@ int main(int argc, char **argv)
         }
         MPI_Bcast(&answer, 1, MPI_INT, 0, MPI_COMM_WORLD);
     } else {
-        s = kth_dist_sample_size(n / P);
+        /* ~kth_dist_sample_size(n) sample keys in all, split over the ranks */
+        s = kth_dist_sample_size(n) / P;
+        s = s < 64 ? 64 : s & ~(int64_t)63;
         HIPCHK(hipMalloc((void **)&d_slots, 3 * (size_t)KTH_STATS_WORDS * 8));
         HIPCHK(hipMalloc((void **)&d_sample, (size_t)s * 4));
         HIPCHK(hipMalloc((void **)&d_sample_all, (size_t)s * 4 * P));

@@ -723,7 +723,7 @@ int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, in
 }
 
 // ------------------------------------------------------- sharded protocol
-int64_t kth_dist_sample_size(int64_t n_local) { return sample_size(n_local); }
+int64_t kth_dist_sample_size(int64_t n) { return sample_size(n); }
 
 int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;

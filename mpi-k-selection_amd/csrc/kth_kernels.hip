@@ -27,8 +27,12 @@ constexpr int MAIN_UNROLL = 8;       // 16-B loads in flight per thread in k_mai
 constexpr int WREG = 1024;            // per-wave candidate staging region (4 KiB LDS)
 constexpr int LEVEL_UNROLL = 8;       // 16-B loads in flight per thread in k_level
 constexpr int DENSE_BLK = 1024;       // workgroup size of the dense-histogram levels
-constexpr int SAMPLE_CHUNK = 64;      // keys per sampled chunk = one wave's 256-B load
-constexpr int GATHER_BATCH = 16;      // sampled chunks in flight per wave
+#ifndef KTH_SAMPLE_CK
+#define KTH_SAMPLE_CK 1
+#endif
+constexpr int SAMPLE_CK = KTH_SAMPLE_CK;            // sampled keys per lane per chunk (1 or 4)
+constexpr int SAMPLE_CHUNK = WAVE * SAMPLE_CK;      // keys per sampled chunk = one wave's load
+constexpr int GATHER_BATCH = 16 / SAMPLE_CK;        // sampled chunks in flight per wave
 constexpr int SMALL_BLOCK = 1024;
 constexpr int ROWS_BLOCK = 256;
 
@@ -385,19 +389,32 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
     const u64 gw = ((u64)blockIdx.x * DENSE_BLK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (DENSE_BLK / WAVE);
     // every wave owns GATHER_BATCH consecutive chunk slots per round; all loads
     // of a round are in flight together (the chunks are 256 KiB apart in HBM)
+    const bool vec = SAMPLE_CK == 4 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0 && stride % 4 == 0;
     for (u64 c0 = gw * GATHER_BATCH; c0 < nchunks; c0 += nw * GATHER_BATCH) {
-        uint32_t kk[GATHER_BATCH];
+        uint32_t kk[GATHER_BATCH][SAMPLE_CK];
 #pragma unroll
         for (int j = 0; j < GATHER_BATCH; ++j) {
             const u64 c = c0 + j;
-            kk[j] = c < nchunks ? key_of_i32((uint32_t)keys[c * stride + lane]) : 0u;
+            const int32_t *src = keys + c * stride + lane * SAMPLE_CK;
+            if (SAMPLE_CK == 4 && vec) {
+                const uint4 x = c < nchunks ? *reinterpret_cast<const uint4 *>(src) : make_uint4(0, 0, 0, 0);
+                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int q = 0; q < SAMPLE_CK; ++q) kk[j][q] = key_of_i32(xs[q & 3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < SAMPLE_CK; ++q) kk[j][q] = c < nchunks ? key_of_i32((uint32_t)src[q]) : 0u;
+            }
         }
 #pragma unroll
         for (int j = 0; j < GATHER_BATCH; ++j) {
             const u64 c = c0 + j;
             if (c < nchunks) {
-                sample[c * SAMPLE_CHUNK + lane] = kk[j];
-                if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j], true);
+#pragma unroll
+                for (int q = 0; q < SAMPLE_CK; ++q) {
+                    sample[c * SAMPLE_CHUNK + lane * SAMPLE_CK + q] = kk[j][q];
+                    if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j][q], true);
+                }
             }
         }
     }

@@ -114,7 +114,9 @@ class DistSelector:
         b = self.b
         if n_total // self.world < SMALL_PER_RANK:
             return self._select_small(shard, n_local, n_total, k)
-        s_local = b.sample_size(n_total // self.world)
+        # the window needs ~sample_size(n_total) sample keys in all (what one GPU
+        # would take), not that many per rank: the all-gather stays ~4 MiB
+        s_local = max(64, (b.sample_size(n_total) // self.world) & ~63)
         if n_local < s_local:
             raise ValueError(f"shard of {n_local} keys is smaller than the per-rank sample ({s_local}); "
                              "use balanced shards (kselect.dist.shard_bounds)")
