@@ -230,6 +230,8 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="global 1-based rank (default n_total/2)")
     ap.add_argument("--cpu-log2n", type=int, default=25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the sharded (kth_dist_* + RCCL) protocol even on one GPU")
     ap.add_argument("--workload", choices=["select", "rows"], default="select",
                     help="select: BASELINE config 2/3 (the metric); rows: config 5, batched k-th per row")
     ap.add_argument("--rows", type=int, default=65536)
@@ -255,8 +257,11 @@ def main():
     # one explicit stream for everything (torch ops, the selector, RCCL): the
     # legacy null stream would add implicit synchronisation to every launch
     torch.cuda.set_stream(torch.cuda.Stream(dev))
+    sharded = world > 1 or args.dist
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    elif args.dist:  # the sharded protocol on one GPU: a one-rank RCCL group
+        dist.init_process_group("nccl", device_id=dev, store=dist.HashStore(), rank=0, world_size=1)
 
     def barrier():
         if world > 1:
@@ -272,7 +277,7 @@ def main():
     sel.fill(keys, n_local, family, args.seed, offset=rank * n_local, n_total=n_total)
     out = torch.zeros(args.warmup + args.steps, dtype=torch.int32, device=dev)
 
-    if world == 1:
+    if not sharded:
         sel.reserve(n_local)
 
         def step(i):
@@ -281,7 +286,7 @@ def main():
         ds = DistSelector(HipBackend(local_rank, sel))
 
         def step(i):
-            out[i:i + 1].copy_(ds.select(keys, n_local, n_total, k))
+            ds.select(keys, n_local, n_total, k, out=out[i:i + 1])
 
     for i in range(args.warmup):
         step(i)
@@ -311,7 +316,7 @@ def main():
         dist.all_reduce(cnt)
     lt, le = (int(x) for x in cnt.tolist())
     verified = (lt < k <= le) and all(a == v for a in answers)
-    stats = sel.stats() if world == 1 else None
+    stats = sel.stats() if not sharded else None
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = n_total / (elapsed / args.steps) / 1e9
@@ -346,7 +351,7 @@ def main():
             "k": k,
             "keys_per_gpu": n_local,
             "family": args.family,
-            "parallelism": f"shards{world}" if world > 1 else "single",
+            "parallelism": f"shards{world}" if sharded else "single",
         },
         "roofline": {
             "bound": "hbm",
@@ -361,7 +366,7 @@ def main():
         },
         "verified": bool(verified),
         "answer": v,
-        "whole_select_ms_events": total_ms / max(1, n_sel) if world == 1 else None,
+        "whole_select_ms_events": total_ms / max(1, n_sel) if not sharded else None,
     }
     if stats:
         res["path"] = {1: "lds", 2: "radix", 3: "window", 4: "window_fallback"}.get(stats["path"], "?")
@@ -383,7 +388,7 @@ def main():
 
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
     return 0 if verified else 1
 

@@ -78,6 +78,8 @@ struct kth_ctx {
     std::vector<hipEvent_t> ev_main, ev_total;
     int main_used = 0, total_used = 0;
     bool dirty = false;  // a launch sequence was cut short: re-zero the slots
+    bool dist_zero = false;  // sharded: the bound slots still need clearing
+    bool dist_open = false;  // sharded: begun, kth_dist_result not yet enqueued
     // KTH_STAMPS=1 diagnostics: per-launch [WG][8] wall-clock stamps, dumped after each select
     u64 *stamps = nullptr;
     int stamp_next = 0;
@@ -732,9 +734,12 @@ int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     c->dist_n = n_total;
     c->dist_k = k;
     c->dist_level_next = 0;
-    HIP_TRY(hipMemsetAsync(d_slots, 0, 3 * (size_t)KTH_STATS_WORDS * 8, c->stream));
-    HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
+    c->dist_zero = true;  // kth_dist_sample clears the slots inside its kernel
+    // the ctx's own slots are left zeroed by every completed k_result; a
+    // sequence cut short (dirty, or a dist selection never finished) re-zeroes
+    if (c->dirty || c->dist_open) HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
     c->dirty = false;
+    c->dist_open = true;
     return KTH_OK;
 }
 
@@ -745,14 +750,24 @@ int kth_dist_sample(kth_ctx *c, const int32_t *d_keys, int64_t n_local, uint32_t
     const u64 stride = (u64)n_local / nchunks;
     StepArgs a;
     memset(&a, 0, sizeof a);
+    if (c->dist_zero && c->uslots) {
+        a.stats_zero = c->uslots;
+        a.zero_words = 3 * (u64)KTH_STATS_WORDS;
+    }
     kth::k_gather<false><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, d_keys, stride, d_sample,
                                                                                 (u64)s_local);
-    return launch_check();
+    KTH_TRY(launch_check());
+    if (a.zero_words) c->dist_zero = false;
+    return KTH_OK;
 }
 
 int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
     if (!c || !d_sample || s_total < 1 || !c->uslots) return KTH_EINVAL;
     KTH_TRY(set_device(c));
+    if (c->dist_zero) {  // no kth_dist_sample since kth_dist_begin (samples from elsewhere)
+        HIP_TRY(hipMemsetAsync(c->uslots, 0, 3 * (size_t)KTH_STATS_WORDS * 8, c->stream));
+        c->dist_zero = false;
+    }
     u64 r_lo, r_hi;
     window_ranks(c->dist_n, c->dist_k, s_total, &r_lo, &r_hi);
     StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
@@ -818,6 +833,7 @@ int kth_dist_result(kth_ctx *c, int32_t *d_out) {
     kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots, ISLOT_WORDS);
     c->last_state = 1 - st_in;
     c->dist_level_next = -1;
+    c->dist_open = false;
     return launch_check();
 }
 

@@ -61,6 +61,7 @@ struct StepArgs {
     u64 init_n, init_k, init_s, r_lo, r_hi;
     u64 min_per_wg;        // keys per active workgroup (sets how many WGs flush a histogram)
     u64 *stamps;           // KTH_STAMPS diagnostics: [gridDim.x][8] wall-clock stamps, else null
+    u64 zero_words;        // k_gather<false> (sharded sample): clear stats_zero[0 .. zero_words)
 };
 
 // Diagnostic phase stamps (KTH_STAMPS=1 only; null pointer in the product):
@@ -383,6 +384,10 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
         publish<DENSE_BLK>(ss, share, a);
         for (int i = threadIdx.x; i < 2 * NBINS; i += DENSE_BLK) (&lh[0][0])[i] = 0;
         __syncthreads();
+    }
+    if (!FUSE) {  // the sharded protocol's slots, cleared here instead of by a memset launch
+        for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < a.zero_words; i += (u64)gridDim.x * DENSE_BLK)
+            a.stats_zero[i] = 0;
     }
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nchunks = s / SAMPLE_CHUNK;

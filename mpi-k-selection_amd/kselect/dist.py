@@ -17,16 +17,20 @@ Replaces the CGM driver of the reference (TODO-kth-problem-cgm.c:76-278):
   :277-278 rank-0 qsort + VecGet(k-1)            one per 11-bit digit (3)
 
 Every rank ends with the same answer (the reference prints it on rank 0 only).
-Collectives are ``torch.distributed`` ops -- RCCL over xGMI with the "nccl"
-backend on ROCm, gloo in the CPU tests -- issued on the current stream, so the
-host never waits between steps.  The per-rank device work is a ``backend``:
+The collectives never make the host wait between steps.  On GPUs they go
+through a direct RCCL communicator on the selector's own stream (kselect.rccl:
+torch's ProcessGroupNCCL would fence every collective with a hop to its
+internal stream); with gloo (CPU tests) they are torch.distributed ops.  The per-rank device work is a ``backend``:
 ``HipBackend`` (libkth.so) in the product; tests plug in a CPU restatement to
 exercise this orchestration on gloo.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check
+from .rccl import RcclComm, TorchComm
 
 SMALL_PER_RANK = 64  # below this many keys per rank: all-gather and select locally
 
@@ -44,8 +48,16 @@ class HipBackend:
     def __init__(self, device, selector=None):
         self.device = torch.device("cuda", device)
         self.sel = selector or Selector(device)
-        self.sel.set_stream(torch.cuda.current_stream(self.device))
+        self.stream = torch.cuda.current_stream(self.device)
+        self.sel.set_stream(self.stream)
         self.ctx = self.sel.handle
+
+    def make_comm(self, group=None):
+        """RCCL on this backend's stream for an "nccl" group (KTH_DIST_COMM=torch
+        forces torch.distributed collectives instead)."""
+        if dist.get_backend(group) == "nccl" and os.environ.get("KTH_DIST_COMM", "rccl") != "torch":
+            return RcclComm(self.device.index, self.stream, group)
+        return TorchComm(group)
 
     def sample_size(self, n_local):
         return int(_lib.kth_dist_sample_size(int(n_local)))
@@ -92,17 +104,21 @@ class HipBackend:
 class DistSelector:
     """k-th smallest of the union of every rank's shard (global 1-based k)."""
 
-    def __init__(self, backend, group=None):
+    def __init__(self, backend, group=None, comm=None):
         self.b = backend
         self.group = group
         self.world = dist.get_world_size(group)
+        if comm is None:
+            comm = backend.make_comm(group) if hasattr(backend, "make_comm") else TorchComm(group)
+        self.comm = comm
         self.slots = backend.alloc_slots()
         self.out = backend.alloc_out()
         self._sample = None
         self._gathered = None
 
-    def select(self, shard, n_local, n_total, k):
-        """Enqueue one selection; returns the device (or CPU, for gloo) int32[1] answer tensor.
+    def select(self, shard, n_local, n_total, k, out=None):
+        """Enqueue one selection; returns the device (or CPU, for gloo) int32[1]
+        answer tensor (``out`` if given, else a buffer reused by every call).
 
         n_total must be the sum of n_local over ranks and k in [1, n_total];
         every rank must pass the same (n_total, k).  Shards are expected to be
@@ -112,8 +128,9 @@ class DistSelector:
         if not (1 <= k <= n_total):
             raise ValueError(f"k={k} outside [1, {n_total}]")
         b = self.b
+        out = self.out if out is None else out
         if n_total // self.world < SMALL_PER_RANK:
-            return self._select_small(shard, n_local, n_total, k)
+            return self._select_small(shard, n_local, n_total, k, out)
         # the window needs ~sample_size(n_total) sample keys in all (what one GPU
         # would take), not that many per rank: the all-gather stays ~4 MiB
         s_local = max(64, (b.sample_size(n_total) // self.world) & ~63)
@@ -125,17 +142,17 @@ class DistSelector:
             self._gathered = b.alloc_sample(s_local * self.world)
         b.begin(self.slots, n_total, k)
         b.sample(shard, n_local, self._sample, s_local)
-        dist.all_gather_into_tensor(self._gathered, self._sample, group=self.group)
+        self.comm.all_gather(self._gathered, self._sample)
         b.window(self._gathered, s_local * self.world)
         i = b.scan(shard, n_local)
-        dist.all_reduce(self.slots[i], op=dist.ReduceOp.SUM, group=self.group)
+        self.comm.all_reduce_sum_(self.slots[i])
         for level in range(KTH_DIST_LEVELS):
             i = b.level(shard, n_local, level)
-            dist.all_reduce(self.slots[i], op=dist.ReduceOp.SUM, group=self.group)
-        b.result(self.out)
-        return self.out
+            self.comm.all_reduce_sum_(self.slots[i])
+        b.result(out)
+        return out
 
-    def _select_small(self, shard, n_local, n_total, k):
+    def _select_small(self, shard, n_local, n_total, k, out):
         """Tiny inputs (cf. the reference's final Gatherv + solve on one rank,
         TODO-kth-problem-cgm.c:235-278): all-gather the shards, select locally."""
         sizes = [torch.zeros(1, dtype=torch.int64, device=self.out.device) for _ in range(self.world)]
@@ -149,5 +166,8 @@ class DistSelector:
         gathered = torch.empty(m * self.world, dtype=torch.int32, device=self.out.device)
         dist.all_gather_into_tensor(gathered, padded, group=self.group)
         union = torch.cat([gathered[r * m:r * m + sizes[r]] for r in range(self.world)])
-        self.b.select_all(union, n_total, k, self.out)
-        return self.out
+        self.b.select_all(union, n_total, k, out)
+        return out
+
+    def close(self):
+        self.comm.close()

@@ -335,13 +335,18 @@ def test_dist_world1_nccl(gpu):
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        ds = DistSelector(HipBackend(0))
-        for fam in ("uniform_full", "few_distinct", "sorted_desc"):
-            n = 1 << 23
-            keys = _dev_keys(gpu, n, fam)
-            srt = np.sort(keys.cpu().numpy())
-            for k in (1, n // 2, n):
-                got = int(ds.select(keys, n, n, k).item())
-                assert got == srt[k - 1], (fam, k)
+        from kselect.rccl import RcclComm, TorchComm
+        b = HipBackend(0)
+        for comm in (None, TorchComm()):  # direct RCCL on the selector's stream (default), torch's
+            ds = DistSelector(b, comm=comm)
+            assert isinstance(ds.comm, RcclComm if comm is None else TorchComm)
+            for fam in ("uniform_full", "few_distinct", "sorted_desc"):
+                n = 1 << 23
+                keys = _dev_keys(gpu, n, fam)
+                srt = np.sort(keys.cpu().numpy())
+                for k in (1, n // 2, n):
+                    got = int(ds.select(keys, n, n, k).item())
+                    assert got == srt[k - 1], (fam, k, type(ds.comm).__name__)
+            ds.close()
     finally:
         dist.destroy_process_group()
