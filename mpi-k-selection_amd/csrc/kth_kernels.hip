@@ -23,8 +23,15 @@
 namespace kth {
 
 constexpr int BLK = 256;
-constexpr int MAIN_UNROLL = 8;       // 16-B loads in flight per thread in k_main
-constexpr int WREG = 1024;            // per-wave candidate staging region (4 KiB LDS)
+#ifndef KTH_MAIN_UNROLL
+#define KTH_MAIN_UNROLL 8
+#endif
+constexpr int MAIN_UNROLL = KTH_MAIN_UNROLL;  // 16-B loads in flight per thread in k_main (multiple of 8)
+constexpr int MAIN_SUB = MAIN_UNROLL < 8 ? MAIN_UNROLL : 8;  // loads per scanned key group
+#ifndef KTH_WREG
+#define KTH_WREG 2048
+#endif
+constexpr int WREG = KTH_WREG;        // per-wave candidate staging region (words of LDS)
 constexpr int LEVEL_UNROLL = 8;       // 16-B loads in flight per thread in k_level
 constexpr int DENSE_BLK = 1024;       // workgroup size of the dense-histogram levels
 #ifndef KTH_SAMPLE_CK
@@ -429,23 +436,17 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
 }
 
 // The streaming pass.  Window [lo, hi] comes from the advance (last sample
-// digit).  Per key: #<lo, #==lo, #==hi in registers.  Keys strictly inside the
-// window are marked in a per-thread bit mask per tile; one wave-wide scan of the
-// per-lane counts places them in the wave's private LDS region (no LDS atomics,
-// no barriers).  A wave flushes its region to the candidate buffer itself, with
-// one global reservation, whenever the next tile might not fit -- so staging
-// never overflows however many keys a workgroup streams.  A single tile with
-// more than WREG candidates (over half its keys inside the window: adversarial
-// input only) is written straight to HBM.
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
-    const int lane = threadIdx.x & (WAVE - 1);
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, WAVE);
-        if (lane >= o) x += y;
-    }
-    return x;
-}
+// digit).  Per key: #<lo, #==lo, #==hi in per-lane registers.  Keys strictly
+// inside the window are staged in the wave's private LDS region one key slot
+// at a time: for slot j the ballot B of the lanes whose j-th key is inside
+// gives each such lane its position (wfill + mbcnt(B)) and advances the
+// wave-uniform fill by popc(B) -- scalar bookkeeping only, no wave scan, no
+// per-lane position chain, no LDS atomics, no barriers (uniform keys: B is
+// empty for ~2/3 of the slots and the branch is skipped).  A wave flushes its
+// region to the candidate buffer itself, with one global reservation, when the
+// next slot might not fit -- so staging never overflows however many keys a
+// workgroup streams.  Candidate order in the buffer is irrelevant (the levels
+// after the pass histogram it as a multiset).
 
 // Reserve `cnt` slots of the candidate buffer for one wave (lane WAVE-1 does the
 // atomic); flags the per-rank overflow word exactly once, on the crossing.
@@ -467,64 +468,76 @@ __device__ __forceinline__ void put_cand(uint32_t *p, uint32_t x) {
     __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Per-tile candidate handling shared by full and ragged tiles.  `cm` has bit j
-// set for key j of this lane's tile inside the window.  One wave scan places
-// the wave's candidates at the end of its LDS region (flushed first if they
-// might not fit); predicated LDS stores write them.
-template <int K>
-__device__ __forceinline__ void stage_tile(const uint32_t (&kk)[K], uint32_t cm, uint32_t *reg, uint32_t &wfill,
-                                           u64 &winside, u64 *cand_count, u64 *acc, u64 cap,
-                                           uint32_t *__restrict__ cand_out) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const uint32_t c = (uint32_t)__popc(cm);
-    const uint32_t incl = wave_inclusive_scan(c);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, WAVE - 1);
-    winside += total;
-    if (wfill + total > (uint32_t)WREG) {  // wave-uniform: flush this wave's region
+struct Stager {
+    uint32_t *reg;       // this wave's LDS region (WREG words)
+    uint32_t wfill;      // wave-uniform fill of the region
+    u64 winside;         // wave-uniform count of candidates seen
+    u64 *cand_count, *acc, cap;
+    uint32_t *cand_out;
+
+    __device__ __forceinline__ void flush() {
         __builtin_amdgcn_wave_barrier();
+        const int lane = threadIdx.x & (WAVE - 1);
         const u64 g = reserve_cands(cand_count, acc, cap, wfill);
         for (uint32_t i = lane; i < wfill; i += WAVE)
             if (g + i < cap) put_cand(&cand_out[g + i], reg[i]);
         __builtin_amdgcn_wave_barrier();
         wfill = 0;
     }
-    if (total > (uint32_t)WREG) {  // adversarial tile (> half its keys inside): straight to HBM
-        u64 g = reserve_cands(cand_count, acc, cap, total) + (incl - c);
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            if (cm & (1u << j)) {
-                if (g < cap) put_cand(&cand_out[g], kk[j]);
-                ++g;
-            }
-        return;
+
+    // One key slot of the wave: `in` = this lane's key is a candidate.
+    __device__ __forceinline__ void slot(uint32_t key, bool in) {
+        const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
+#ifdef KTH_DIAG_NOSTAGE
+        if (B == 0x123456789ull) {  // diagnostic build only: measures the staging cost
+#else
+        if (B) {  // wave-uniform
+#endif
+            const uint32_t nb = (uint32_t)__popcll(B);
+            if (wfill + nb > (uint32_t)WREG) flush();
+            const uint32_t below =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+            if (in) reg[wfill + below] = key;
+            wfill += nb;
+            winside += nb;
+        }
     }
-    uint32_t pos = wfill + incl - c;
+};
+
+// Count and stage K keys of this lane (key j valid iff bit j of `valid`).  The
+// keys are the raw int32 words: signed compares against the signed window
+// bounds order them exactly like the order-preserving keys (no per-key xor);
+// only a staged candidate is converted.
+template <int K, bool FULL>
+__device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t valid, int32_t slo, int32_t shi,
+                                          uint32_t &clt, uint32_t &ceqlo, uint32_t &ceqhi, Stager &st) {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        if (cm & (1u << j)) reg[pos++] = kk[j];
-    wfill += total;
+    for (int j = 0; j < K; ++j) {
+        const int32_t x = (int32_t)xw[j];
+        const bool ok = FULL || ((valid >> j) & 1u);
+        clt += (ok & (x < slo)) ? 1u : 0u;
+        ceqlo += (ok & (x == slo)) ? 1u : 0u;
+        ceqhi += (ok & (x == shi)) ? 1u : 0u;
+        st.slot((uint32_t)x ^ 0x80000000u, ok & (x > slo) & (x < shi));
+    }
 }
 
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out) {
-    constexpr int U = MAIN_UNROLL, K = 4 * U;
+    constexpr int U = MAIN_UNROLL, S = MAIN_SUB, K = 4 * S;
+    static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
     __shared__ u64 scratch[BLK / WAVE + 4];
     __shared__ uint32_t region[BLK / WAVE][WREG];
-    __shared__ u64 red[4][BLK / WAVE];
+    __shared__ u64 red[6][BLK / WAVE];
     KTH_STAMP(a, 0);
     advance<BLK>(ss, a, scratch);
     publish<BLK>(ss, 0, a);
     KTH_STAMP(a, 1);
     if (ss.mode != MODE_MAIN) return;  // block-uniform (error or resolved)
-    const uint32_t lo = ss.lo, hi = ss.hi;
-    const u64 cap = a.cap;
-    u64 *const cand_count = a.cand_count;
-    u64 *const acc = a.stats_acc;
+    const int32_t slo = i32_of_key(ss.lo), shi = i32_of_key(ss.hi);
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
-    uint32_t *const reg = region[wid];
+    Stager st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
-    uint32_t wfill = 0;                      // wave-uniform
-    u64 winside = 0;                         // wave-uniform
 
     const uint32_t *p = reinterpret_cast<const uint32_t *>(a.keys);
     const u64 n = a.n_local;
@@ -533,86 +546,59 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(p + head);
     const u64 nv = (n - head) >> 2, tail0 = head + (nv << 2);
     const u64 tile = (u64)BLK * U, nfull = nv / tile;
-    // full tiles: grid-strided, every load of a tile issued before any use
-    for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
+    // full tiles: grid-strided; the tile is consumed in groups of 4 * MAIN_SUB keys
+    auto load_tile = [&](uint4 (&x)[U], u64 t) {
         const uint4 *src = v + t * tile + threadIdx.x;
-        uint4 x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
-        uint32_t kk[K];
-        uint32_t cm = 0;
+    };
+    auto scan_tile = [&](const uint4 (&x)[U]) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            kk[4 * u + 0] = x[u].x ^ 0x80000000u;
-            kk[4 * u + 1] = x[u].y ^ 0x80000000u;
-            kk[4 * u + 2] = x[u].z ^ 0x80000000u;
-            kk[4 * u + 3] = x[u].w ^ 0x80000000u;
-        }
+        for (int h = 0; h < U / S; ++h) {
+            uint32_t kk[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const uint32_t key = kk[j];
-            clt += key < lo;
-            ceqlo += key == lo;
-            ceqhi += key == hi;
-            cm |= ((key > lo) & (key < hi)) ? (1u << j) : 0u;
+            for (int u = 0; u < S; ++u) {
+                kk[4 * u + 0] = x[h * S + u].x;
+                kk[4 * u + 1] = x[h * S + u].y;
+                kk[4 * u + 2] = x[h * S + u].z;
+                kk[4 * u + 3] = x[h * S + u].w;
+            }
+            scan_keys<K, true>(kk, 0xFFFFFFFFu, slo, shi, clt, ceqlo, ceqhi, st);
         }
-        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
+    };
+    // every load of a tile issued before any use
+    for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
+        uint4 x[U];
+        load_tile(x, t);
+        scan_tile(x);
     }
-    // ragged end: the last partial tile, as one masked tile of one workgroup
+    // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;
-    if (blockIdx.x == (uint32_t)(nfull % gridDim.x)) {
-        uint32_t kk[K];
-        uint32_t ok = 0;
+    if (blockIdx.x == (uint32_t)(nfull % gridDim.x))
+        for (int h = 0; h < U / S; ++h) {
+            uint32_t kk[K];
+            uint32_t ok = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const u64 i = rem0 + u * BLK + threadIdx.x;
-            const bool in = i < nv;
-            const uint4 x = in ? v[i] : make_uint4(0, 0, 0, 0);
-            kk[4 * u + 0] = x.x ^ 0x80000000u;
-            kk[4 * u + 1] = x.y ^ 0x80000000u;
-            kk[4 * u + 2] = x.z ^ 0x80000000u;
-            kk[4 * u + 3] = x.w ^ 0x80000000u;
-            ok |= in ? (0xFu << (4 * u)) : 0u;
+            for (int u = 0; u < S; ++u) {
+                const u64 i = rem0 + (h * S + u) * BLK + threadIdx.x;
+                const bool in = i < nv;
+                const uint4 x = in ? v[i] : make_uint4(0, 0, 0, 0);
+                kk[4 * u + 0] = x.x;
+                kk[4 * u + 1] = x.y;
+                kk[4 * u + 2] = x.z;
+                kk[4 * u + 3] = x.w;
+                ok |= in ? (0xFu << (4 * u)) : 0u;
+            }
+            scan_keys<K, false>(kk, ok, slo, shi, clt, ceqlo, ceqhi, st);
         }
-        uint32_t cm = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const uint32_t key = kk[j];
-            const bool in = (ok >> j) & 1u;
-            clt += (in & (key < lo)) ? 1u : 0u;
-            ceqlo += (in & (key == lo)) ? 1u : 0u;
-            ceqhi += (in & (key == hi)) ? 1u : 0u;
-            cm |= (in & (key > lo) & (key < hi)) ? (1u << j) : 0u;
-        }
-        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
-    }
     if (blockIdx.x == 0) {  // the < 4-key unaligned head and tail
-        uint32_t kk[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) kk[j] = 0;
         const bool okh = threadIdx.x < head, okt = threadIdx.x < n - tail0;
-        kk[0] = (okh ? p[threadIdx.x] : 0u) ^ 0x80000000u;
-        kk[1] = (okt ? p[tail0 + threadIdx.x] : 0u) ^ 0x80000000u;
-        const uint32_t ok = (okh ? 1u : 0u) | (okt ? 2u : 0u);
-        uint32_t cm = 0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t key = kk[j];
-            const bool in = (ok >> j) & 1u;
-            clt += (in & (key < lo)) ? 1u : 0u;
-            ceqlo += (in & (key == lo)) ? 1u : 0u;
-            ceqhi += (in & (key == hi)) ? 1u : 0u;
-            cm |= (in & (key > lo) & (key < hi)) ? (1u << j) : 0u;
-        }
-        if (__ballot(cm != 0)) stage_tile<K>(kk, cm, reg, wfill, winside, cand_count, acc, cap, cand_out);
+        const uint32_t kk[2] = {okh ? p[threadIdx.x] : 0u, okt ? p[tail0 + threadIdx.x] : 0u};
+        scan_keys<2, false>(kk, (okh ? 1u : 0u) | (okt ? 2u : 0u), slo, shi, clt, ceqlo, ceqhi, st);
     }
-    if (wfill) {  // final flush of this wave's region
-        __builtin_amdgcn_wave_barrier();
-        const u64 g = reserve_cands(cand_count, acc, cap, wfill);
-        for (uint32_t i = lane; i < wfill; i += WAVE)
-            if (g + i < cap) put_cand(&cand_out[g + i], reg[i]);
-    }
-    // counts: wave reduce -> LDS -> one atomic per workgroup and counter
+    // counts: wave reduce -> LDS -> one atomic per workgroup and counter; the
+    // waves' final region fills are combined the same way, so the candidate
+    // buffer sees one reservation per workgroup at the end of the pass
     u64 r0 = clt, r1 = ceqlo, r2 = ceqhi;
 #pragma unroll
     for (int o = WAVE / 2; o > 0; o >>= 1) {
@@ -624,14 +610,31 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         red[0][wid] = r0;
         red[1][wid] = r1;
         red[2][wid] = r2;
-        red[3][wid] = winside;
+        red[3][wid] = st.winside;
+        red[4][wid] = st.wfill;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < 5) {
         u64 sum = 0;
         for (int w = 0; w < BLK / WAVE; ++w) sum += red[threadIdx.x][w];
-        const int slot[4] = {C_LT, C_EQLO, C_EQHI, C_IN};
-        if (sum) atomicAdd(&acc[slot[threadIdx.x]], sum);
+        if (threadIdx.x == 4) {
+            u64 g = 0;
+            if (sum) {
+                g = atomicAdd(a.cand_count, sum);
+                if (g <= a.cap && g + sum > a.cap) atomicAdd(&a.stats_acc[C_OVF], 1ull);
+            }
+            red[5][0] = g;
+        } else {
+            const int slot[4] = {C_LT, C_EQLO, C_EQHI, C_IN};
+            if (sum) atomicAdd(&a.stats_acc[slot[threadIdx.x]], sum);
+        }
+    }
+    __syncthreads();
+    if (st.wfill) {  // this wave's final region, at its share of the reservation
+        u64 g = red[5][0];
+        for (int w = 0; w < wid; ++w) g += red[4][w];
+        for (uint32_t i = lane; i < st.wfill; i += WAVE)
+            if (g + i < a.cap) put_cand(&cand_out[g + i], st.reg[i]);
     }
     KTH_STAMP(a, 5);
 }
