@@ -384,11 +384,14 @@ thread_local kth_ctx *tl_ctx = nullptr;
 template <bool F32, int KPL, bool TOPK>
 void launch_rows_reg(kth_ctx *c, bool vec, int g, const uint32_t *d_keys, u64 R, uint32_t C, uint32_t K,
                      uint32_t *d_out, uint32_t flip, uint32_t *vals, int32_t *idx) {
-    if (vec)
-        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0, TOPK>
+    if (vec && C == (uint32_t)(KPL * kth::WAVE))
+        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0, TOPK, true>
+            <<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out, flip, vals, idx);
+    else if (vec)
+        kth::k_rows_reg<F32, KPL, true, KTH_ROWS_R0, TOPK, false>
             <<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out, flip, vals, idx);
     else
-        kth::k_rows_reg<F32, KPL, false, KTH_ROWS_R0, TOPK>
+        kth::k_rows_reg<F32, KPL, false, KTH_ROWS_R0, TOPK, false>
             <<<g, kth::RW_BLOCK, 0, c->stream>>>(d_keys, R, C, K, d_out, flip, vals, idx);
 }
 

@@ -21,8 +21,17 @@
 namespace kth {
 
 constexpr int RW_BLOCK = 256;
+#ifndef KTH_ROWS_WAVES
+#define KTH_ROWS_WAVES 4  // waves per SIMD the register budget is held to (<= 128 VGPRs)
+#endif
 constexpr int RW_BINS = 256;
-constexpr int RW_STRIDE = RW_BINS + 1;  // words between histogram copies
+constexpr int RW_STRIDE = RW_BINS + 4;  // words between histogram copies: 16-B aligned, a bin's copies in different banks
+
+// Zero bins 0..255 of `copies` histogram copies: one 16-byte store per lane per copy.
+__device__ __forceinline__ void zero_hist(uint32_t *hist, int copies, int lane) {
+    for (int c = 0; c < copies; ++c)
+        reinterpret_cast<uint4 *>(hist + c * RW_STRIDE)[lane] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 // Raw bits of a key (inverse of the order-preserving transform).
 template <bool F32>
@@ -30,23 +39,473 @@ __device__ __forceinline__ uint32_t raw_of_key(uint32_t key) {
     return F32 ? f32_of_key(key) : (uint32_t)i32_of_key(key);
 }
 
+// Cross-lane steps on DPP (row shifts and row broadcasts) and readlane: no
+// LDS round trip and no per-lane address registers (__shfl's bpermute
+// addresses are loop-invariant, get hoisted out of the row loop and spilled).
+constexpr int DPP_ROW_SHR = 0x110, DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143;
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWS, 0xF, false);
+}
+
+// Inclusive prefix sum over the wave (lane 63 holds the total).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += dpp<DPP_ROW_SHR + 1, 0xF>(0u, x);
+    x += dpp<DPP_ROW_SHR + 2, 0xF>(0u, x);
+    x += dpp<DPP_ROW_SHR + 4, 0xF>(0u, x);
+    x += dpp<DPP_ROW_SHR + 8, 0xF>(0u, x);
+    x += dpp<DPP_BCAST15, 0xA>(0u, x);
+    x += dpp<DPP_BCAST31, 0xC>(0u, x);
+    return x;
+}
+
+// Wave-wide reduction, result wave-uniform (op(a, b) commutative; id its identity).
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t x, uint32_t id, Op op) {
+    x = op(x, dpp<DPP_ROW_SHR + 1, 0xF>(id, x));
+    x = op(x, dpp<DPP_ROW_SHR + 2, 0xF>(id, x));
+    x = op(x, dpp<DPP_ROW_SHR + 4, 0xF>(id, x));
+    x = op(x, dpp<DPP_ROW_SHR + 8, 0xF>(id, x));
+    x = op(x, dpp<DPP_BCAST15, 0xA>(id, x));
+    x = op(x, dpp<DPP_BCAST31, 0xC>(id, x));
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+__device__ __forceinline__ uint32_t lane_val(uint32_t x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ u64 lane_val(u64 x, int l) {
+    return ((u64)lane_val((uint32_t)(x >> 32), l) << 32) | lane_val((uint32_t)x, l);
+}
+
+// Pick the bin holding the kk-th key from a wave-private 256-bin histogram
+// (`copies` copies RW_STRIDE words apart): lane l owns bins 4l..4l+3; one wave
+// scan of the per-lane sums and a ballot find the bin.  Returns the bin, the
+// keys in bins below it and the keys in it (wave-uniform).
+__device__ __forceinline__ void wave_pick(const uint32_t *hist, int copies, int lane, uint32_t kk, uint32_t &bin,
+                                          uint32_t &below, uint32_t &cnt) {
+    uint32_t h[4] = {0u, 0u, 0u, 0u};
+    for (int c = 0; c < copies; ++c) {
+        const uint4 b = reinterpret_cast<const uint4 *>(hist + c * RW_STRIDE)[lane];
+        h[0] += b.x;
+        h[1] += b.y;
+        h[2] += b.z;
+        h[3] += b.w;
+    }
+    const uint32_t sum = h[0] + h[1] + h[2] + h[3];
+    const uint32_t incl = wave_incl_scan(sum);
+    const uint32_t excl = incl - sum;
+    const unsigned long long bm = __ballot(kk > excl && kk <= incl);
+    const int L = bm ? __ffsll((long long)bm) - 1 : 0;
+    uint32_t b = 0, bl = excl, c = 0;
+    if (lane == L) {
+        bool f = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!f && bl + h[q] >= kk) {
+                b = (uint32_t)(4 * L + q);
+                c = h[q];
+                f = true;
+            } else if (!f) {
+                bl += h[q];
+            }
+        }
+    }
+    bin = lane_val(b, L);
+    below = lane_val(bl, L);
+    cnt = lane_val(c, L);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    return wave_reduce(x, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return min(a, b); });
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    return wave_reduce(x, 0u, [](uint32_t a, uint32_t b) { return max(a, b); });
+}
+
+// An opaque copy of a wave-uniform value: per-key expressions built on it are
+// neither hoisted out of a loop nor shared with an earlier loop, which would
+// keep one extra VGPR per key live (the keys already take KPL of them).
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    uint32_t y;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(y) : "s"(__builtin_amdgcn_readfirstlane(x)));
+    return y;
+}
+__device__ __forceinline__ float opaque(float x) { return __uint_as_float(opaque(__float_as_uint(x))); }
+
+// The first kernel's selection (A/B reference, KTH_ROWS_LEGACY): four 8-bit
+// radix digits of the raw order key, the first counted into R0 copies.
+// Returns the kk-th smallest of the lane keys; kk becomes its rank among the
+// keys equal to it.
+template <int KPL, int R0>
+__device__ __forceinline__ uint32_t row_select_radix(const uint32_t (&key)[KPL], uint32_t *hist, int lane,
+                                                     uint32_t &kk) {
+    uint32_t prefix = 0;
+    for (int pass = 0; pass < 4; ++pass) {  // wave-uniform
+        const int shift = 24 - 8 * pass;
+        const uint32_t pmask = pass ? 0xFFFFFFFFu << (32 - 8 * pass) : 0u;
+        const int copies = pass ? 1 : R0;
+        zero_hist(hist, copies, lane);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t *mine = hist + (pass ? 0 : (lane % R0) * RW_STRIDE);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j)
+            if ((key[j] & pmask) == prefix) atomicAdd(&mine[(key[j] >> shift) & 0xFFu], 1u);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t bin, below, cnt;
+        wave_pick(hist, copies, lane, kk, bin, below, cnt);
+        kk -= below;
+        prefix |= bin << shift;
+        __builtin_amdgcn_wave_barrier();  // the next zeroing after every lane's histogram reads
+        if (cnt == 1 && pass < 3) {  // the single key with this prefix is the answer
+            const uint32_t nmask = 0xFFFFFFFFu << shift;
+            uint32_t val = 0;
+            bool have = false;
+#pragma unroll
+            for (int j = 0; j < KPL; ++j)
+                if (!have && (key[j] & nmask) == prefix) {
+                    val = key[j];
+                    have = true;
+                }
+            const unsigned long long hm = __ballot(have);
+            return lane_val(val, __ffsll((long long)hm) - 1);
+        }
+    }
+    return prefix;
+}
+
+// Float value of an order key in the selection order (ascending; for flip =
+// ~0, the negated value, so that it ascends as the flipped keys do).
+__device__ __forceinline__ float sel_value(uint32_t x, uint32_t flip) {
+    const uint32_t key = x ^ flip;
+    const uint32_t raw = (key & 0x80000000u) ? (key & 0x7FFFFFFFu) : ~key;
+    const float v = __uint_as_float(raw);
+    return flip ? -v : v;
+}
+
+// Range-normalised selection.  Pass A buckets every key by a monotone
+// (non-decreasing) map b(x) into 256 bins spanning the row's own [kmin, kmax]:
+//   int keys / non-finite float rows: b(x) = min(255, (x - kmin) >> sh), the
+//       top 8 bits of the row's key range;
+//   finite float rows: b(x) = min(255, (value(x) - vmin) * 256 / (vmax - vmin)),
+//       linear in the VALUE, so uniform floats fill the bins evenly instead of
+//       piling onto a few exponent bytes (LDS atomics on one address serialise).
+// Rounding of the float map is monotone, so b is monotone and the keys of the
+// picked bin B are exactly the keys of one interval [amin, amax]: the later
+// passes are 8-bit radix digits of x - amin over that interval only.  Exact
+// for any input; only the speed depends on the distribution.  Padding keys
+// (0xFFFFFFFF, past `cols`) sort last and are bucketed like any key (the float
+// map clamps them to bin 255); since k <= cols they never become the answer.
+template <bool F32, int KPL, int R0>
+__device__ __forceinline__ uint32_t row_select_range(const uint32_t (&key)[KPL], uint32_t *hist, int lane,
+                                                     uint32_t &kk, uint32_t cols, uint32_t flip) {
+    // the row's valid key range (padding excluded)
+    uint32_t lmin = 0xFFFFFFFFu, lmax = 0u;
+    const bool ragged = cols != (uint32_t)(KPL * WAVE);
+    if (!ragged) {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            lmin = min(lmin, key[j]);
+            lmax = max(lmax, key[j]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const uint32_t e = (uint32_t)((j / 4) * WAVE + lane) * 4u + (j & 3);
+            lmin = min(lmin, key[j]);
+            lmax = max(lmax, e < cols ? key[j] : 0u);
+        }
+    }
+    const uint32_t kmin = wave_min_u32(lmin), kmax = wave_max_u32(lmax);
+    if (kmin == kmax) return kmin;  // kk is the rank among equal keys already
+
+    // ---- pass A
+    bool fmap = false;
+    float fs = 0.f, fo = 0.f;
+    if (F32) {
+        const float vmin = sel_value(kmin, flip), vmax = sel_value(kmax, flip);
+        const float range = vmax - vmin;
+        const float scale = 256.0f / range;
+        fmap = __builtin_isfinite(vmin) && __builtin_isfinite(vmax) && __builtin_isfinite(range) && range > 0.f &&
+               __builtin_isfinite(scale) && scale > 0.f;
+        fs = scale;
+        fo = vmin;
+    }
+    const uint32_t span0 = kmax - kmin;
+    const uint32_t W0 = 32u - (uint32_t)__clz(span0);
+    const uint32_t sh = W0 > 8u ? W0 - 8u : 0u;
+    // b(x); the parameters are passed in so that a second evaluation can take
+    // opaque copies (no per-key values shared between the two loops)
+    auto bucket = [&](uint32_t x, uint32_t lo, uint32_t hi, uint32_t shf, float o, float sc, uint32_t fl) -> uint32_t {
+        if (F32 && fmap) {
+            const float t = (sel_value(x, fl) - o) * sc;
+            const uint32_t b = (uint32_t)__builtin_amdgcn_fmed3f(t, 0.f, 255.f);
+            return x > hi ? 255u : b;
+        }
+        return min(255u, (x - lo) >> shf);
+    };
+    zero_hist(hist, R0, lane);
+    __builtin_amdgcn_wave_barrier();
+    {
+        uint32_t *mine = hist + (lane % R0) * RW_STRIDE;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) atomicAdd(&mine[bucket(key[j], kmin, kmax, sh, fo, fs, flip)], 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t bin, below, cnt;
+    wave_pick(hist, R0, lane, kk, bin, below, cnt);
+    kk -= below;
+    __builtin_amdgcn_wave_barrier();  // later zeroing after every lane's reads
+
+    // ---- the picked bin as an interval [base, base + span], digits done so far
+    uint32_t base, span, W, done, prefix;
+    if (F32 && fmap) {
+        uint32_t amin = 0xFFFFFFFFu, amax = 0u;
+        const float o2 = opaque(fo), s2 = opaque(fs);
+        const uint32_t hi2 = opaque(kmax), fl2 = opaque(flip);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const bool in = bucket(key[j], kmin, hi2, sh, o2, s2, fl2) == bin;
+            amin = in ? min(amin, key[j]) : amin;
+            amax = in ? max(amax, key[j]) : amax;
+        }
+        amin = wave_min_u32(amin);
+        amax = wave_max_u32(amax);
+        if (amin == amax) return amin;
+        base = amin;
+        span = amax - amin;
+        W = 32u - (uint32_t)__clz(span);
+        done = 0;
+        prefix = 0;
+        cnt = 0;  // unknown as an interval count: run at least one digit
+    } else {
+        base = kmin;
+        span = span0;
+        W = W0;
+        done = W0 - sh;
+        prefix = bin;
+    }
+    // ---- 8-bit digits of x - base over the live interval
+    while (true) {  // wave-uniform
+        const uint32_t ob = opaque(base);
+        auto live = [&](uint32_t x, uint32_t dn, uint32_t pf) {
+            const uint32_t v = x - ob;
+            return v <= span && (dn == 0 || (v >> (W - dn)) == pf);
+        };
+        if (done == W) return ob + prefix;
+        if (cnt == 1) {  // the single live key is the answer
+            uint32_t val = 0;
+            bool have = false;
+#pragma unroll
+            for (int j = 0; j < KPL; ++j)
+                if (!have && live(key[j], done, prefix)) {
+                    val = key[j];
+                    have = true;
+                }
+            const unsigned long long hm = __ballot(have);
+            return lane_val(val, __ffsll((long long)hm) - 1);
+        }
+        const uint32_t d = min(8u, W - done);
+        const uint32_t s = W - done - d, m = (1u << d) - 1u;
+        zero_hist(hist, 1, lane);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < KPL; ++j)
+            if (live(key[j], done, prefix)) atomicAdd(&hist[((key[j] - ob) >> s) & m], 1u);
+        __builtin_amdgcn_wave_barrier();
+        wave_pick(hist, 1, lane, kk, bin, below, cnt);
+        kk -= below;
+        prefix = (prefix << d) | bin;
+        done += d;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// v_min3_f32 / v_max3_f32 without the IEEE-mode input canonicalisation the
+// compiler adds around fminf/fmaxf (the row is NaN-checked separately).
+__device__ __forceinline__ float min3f(float a, float b, float c) {
+    float d;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float d;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// Value-linear bin of a finite float: clamp(fma(v, s, o), 0, 255).  fma and
+// the clamp are monotone (rounding is), so the bin is a non-decreasing
+// function of v, hence of the order key.
+__device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
+    return (uint32_t)__builtin_amdgcn_fmed3f(__builtin_fmaf(v, s, o), 0.f, 255.f);
+}
+
+// Fast path for full rows (cols = 64 * KPL, 16-byte aligned): one histogram
+// pass, then the keys of the picked bin go to an LDS list and are ranked there.
+//   pass A: 256 bins of a monotone map b(x) -- the top byte of the order key
+//       (int32, and float rows holding a NaN or an infinity), or for finite
+//       float rows a bin LINEAR IN THE VALUE over the row's own [vmin, vmax]
+//       (vbin), so uniform floats fill the bins evenly instead of piling onto
+//       a few exponent bytes.  Float keys stay raw bits until they are needed
+//       as order keys;
+//   filter: the keys of the picked bin B (same b, recomputed) are appended to
+//       the wave's LDS list (ballot + mbcnt, only on the slots where some lane
+//       has one);
+//   rank: with L <= 64 listed keys, lane i ranks list[i] against the list.
+// b is monotone, so the bin's keys are exactly the keys between two order
+// keys, and the kk-th of the row is the kk-th (after the keys below B) of the
+// list.  A bin of more than 64 keys (duplicate-heavy or clustered rows) goes
+// to the masked radix sweeps of row_select_radix.  Per key: ~5 VALU ops
+// (int32) / ~11 (float) and one LDS atomic.  On return key[] holds order keys
+// (xor flip) when KEYS_OUT (top-k compaction); else float rows may keep raw bits.
+template <bool F32, int KPL, int R0, bool KEYS_OUT>
+__device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
+                                                    uint32_t flip) {
+    auto to_keys = [&]() {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            asm volatile("" : "+v"(key[j]));  // no sharing with earlier conversions (one live copy)
+            key[j] = key_of_f32(key[j]) ^ flip;
+        }
+    };
+    bool fmap = false;
+    float fs = 0.f, fo = 0.f;
+    if (F32) {  // key[] holds raw float bits
+        float vmin = __uint_as_float(key[0]), vmax = vmin;
+        uint32_t amax = 0;  // largest |bits| << 1: > 0xFF000000 iff a NaN, == iff an infinity
+#pragma unroll
+        for (int j = 0; j < KPL; j += 2) {
+            const float a = __uint_as_float(key[j]), b = __uint_as_float(key[j + 1]);
+            vmin = min3f(vmin, a, b);
+            vmax = max3f(vmax, a, b);
+            amax = max(amax, max(key[j] << 1, key[j + 1] << 1));
+        }
+        amax = wave_max_u32(amax);
+        vmin = __uint_as_float(wave_reduce(__float_as_uint(vmin), 0x7F800000u, [](uint32_t a, uint32_t b) {
+            return __float_as_uint(min3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
+        }));
+        vmax = __uint_as_float(wave_reduce(__float_as_uint(vmax), 0xFF800000u, [](uint32_t a, uint32_t b) {
+            return __float_as_uint(max3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
+        }));
+        const float range = vmax - vmin, scale = 256.0f / range;
+        fmap = amax < 0xFF000000u && __builtin_isfinite(range) && range > 0.f && __builtin_isfinite(scale) &&
+               scale > 0.f;
+        // bins ascend with the selection order: ascending v (flip = 0) or descending
+        fs = flip ? -scale : scale;
+        fo = flip ? vmax * scale : -vmin * scale;
+        fs = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fs)));
+        fo = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fo)));
+        if (!fmap) to_keys();
+    }
+    const bool vmap = F32 && fmap;
+    zero_hist(hist, R0, lane);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t *mine = hist + (lane % R0) * RW_STRIDE;
+    if (vmap) {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) atomicAdd(&mine[vbin(__uint_as_float(key[j]), fs, fo)], 1u);
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) atomicAdd(&mine[key[j] >> 24], 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t bin, below, cnt;
+    wave_pick(hist, R0, lane, kk, bin, below, cnt);
+    __builtin_amdgcn_wave_barrier();  // every lane's histogram reads before the list overwrites it
+    if (cnt > (uint32_t)WAVE) {
+        if (vmap) to_keys();
+        return row_select_radix<KPL, R0>(key, hist, lane, kk);
+    }
+    kk -= below;
+
+    // filter the bin's keys into the list (the histogram words)
+    // vbin(v) == B  <=>  B <= t < B + 1 for t = fma(v, s, o) (the clamp only
+    // merges t < 0 into bin 0 and t >= 255 into bin 255): one fma, two compares
+    const float s2 = opaque(fs), o2 = opaque(fo);  // recompute t, do not keep the bins
+    const float tlo = bin ? (float)bin : -__builtin_inff(), thi = bin < 255u ? (float)(bin + 1) : __builtin_inff();
+    const uint32_t lo = opaque(bin << 24);  // top-byte bin B = keys [B << 24, +2^24)
+    uint32_t fill = 0;
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        bool in;
+        if (vmap) {
+            const float t = __builtin_fmaf(__uint_as_float(key[j]), s2, o2);
+            in = t >= tlo && t < thi;
+        } else {
+            in = key[j] - lo <= 0x00FFFFFFu;
+        }
+        const unsigned long long B = __ballot(in);
+        if (B) {  // wave-uniform
+            const uint32_t pos =
+                fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+            if (in) hist[pos] = key[j];
+            fill += (uint32_t)__popcll(B);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t L = cnt;  // == fill
+    if (vmap) {  // raw bits -> order keys, in the list
+        if ((uint32_t)lane < L) hist[lane] = key_of_f32(hist[lane]) ^ flip;
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t my = (uint32_t)lane < L ? hist[lane] : 0u;
+    uint32_t lt = 0, le = 0;
+    for (uint32_t i = 0; i < L; ++i) {  // wave-uniform trip count, broadcast reads
+        const uint32_t y = hist[i];
+        lt += y < my ? 1u : 0u;
+        le += y <= my ? 1u : 0u;
+    }
+    const unsigned long long bm = __ballot((uint32_t)lane < L && lt < kk && kk <= le);
+    const int f = bm ? __ffsll((long long)bm) - 1 : 0;
+    const uint32_t answer = lane_val(my, f);
+    kk -= lane_val(lt, f);
+    __builtin_amdgcn_wave_barrier();
+    if (KEYS_OUT && vmap) to_keys();
+    return answer;
+}
+
 // TOPK = false: out[r] = the k-th smallest of row r.
 // TOPK = true: vals[r*k ..] / idx[r*k ..] = the k smallest keys of row r and
 // their columns, in column order; of the keys equal to the k-th, the first
 // ones by column.  flip = 0xFFFFFFFF selects the k largest instead (the key
 // order reversed: ~key).
-template <bool F32, int KPL, bool VEC, int R0, bool TOPK>
-__global__ __launch_bounds__(RW_BLOCK) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
+// FULL: cols == 64 * KPL and 16-byte aligned rows (unguarded loads, row_select_fast).
+template <bool F32, int KPL, bool VEC, int R0, bool TOPK, bool FULL>
+__global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
                                                       uint32_t k, uint32_t *__restrict__ out, uint32_t flip,
                                                       uint32_t *__restrict__ vals, int32_t *__restrict__ idx) {
     static_assert(KPL % 4 == 0, "16-byte loads");
-    __shared__ uint32_t hist_all[RW_BLOCK / WAVE][R0 * RW_STRIDE];
+    __shared__ __attribute__((aligned(16))) uint32_t hist_all[RW_BLOCK / WAVE][R0 * RW_STRIDE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     uint32_t *hist = hist_all[wid];
     const u64 wave0 = (u64)blockIdx.x * (RW_BLOCK / WAVE) + wid, nwaves = (u64)gridDim.x * (RW_BLOCK / WAVE);
     for (u64 r = wave0; r < rows; r += nwaves) {  // wave-uniform
         const uint32_t *row = m + r * (u64)cols;
         uint32_t key[KPL];
+        uint32_t kk = k, answer;
+        if (FULL) {
+#pragma unroll
+            for (int j = 0; j < KPL / 4; ++j) {
+                const uint4 x = load_nt(reinterpret_cast<const uint4 *>(row + (j * WAVE + lane) * 4));
+                key[4 * j + 0] = x.x;
+                key[4 * j + 1] = x.y;
+                key[4 * j + 2] = x.z;
+                key[4 * j + 3] = x.w;
+            }
+            if (!F32) {
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) key[j] = key_of_i32(key[j]) ^ flip;
+            }
+#ifdef KTH_ROWS_LEGACY
+            if (F32) {
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) key[j] = key_of_f32(key[j]) ^ flip;
+            }
+            answer = row_select_radix<KPL, R0>(key, hist, lane, kk);
+#else
+            answer = row_select_fast<F32, KPL, R0, TOPK>(key, hist, lane, kk, TOPK ? flip : 0u);
+#endif
+        } else {
 #pragma unroll
         for (int j = 0; j < KPL / 4; ++j) {
             const uint32_t e = (uint32_t)(j * WAVE + lane) * 4u;  // first element of this lane's vector j
@@ -64,72 +523,12 @@ __global__ __launch_bounds__(RW_BLOCK) void k_rows_reg(const uint32_t *__restric
             for (int q = 0; q < 4; ++q)
                 key[4 * j + q] = e + q < cols ? ((F32 ? key_of_f32(v[q]) : key_of_i32(v[q])) ^ flip) : 0xFFFFFFFFu;
         }
-        uint32_t prefix = 0, kk = k, answer = 0;
-        bool found = false;
-        for (int pass = 0; pass < 4; ++pass) {  // wave-uniform
-            const int shift = 24 - 8 * pass;
-            const uint32_t pmask = pass ? 0xFFFFFFFFu << (32 - 8 * pass) : 0u;
-            const int copies = pass ? 1 : R0;
-            for (int i = lane; i < copies * RW_STRIDE; i += WAVE) hist[i] = 0;
-            __builtin_amdgcn_wave_barrier();
-            uint32_t *mine = hist + (pass ? 0 : (lane % R0) * RW_STRIDE);
-#pragma unroll
-            for (int j = 0; j < KPL; ++j)
-                if ((key[j] & pmask) == prefix) atomicAdd(&mine[(key[j] >> shift) & 0xFFu], 1u);
-            __builtin_amdgcn_wave_barrier();
-            uint32_t h[4] = {0u, 0u, 0u, 0u};  // bins 4*lane .. 4*lane + 3, summed over the copies
-            for (int c = 0; c < copies; ++c) {
-                const uint32_t *b = hist + c * RW_STRIDE + 4 * lane;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) h[q] += b[q];
-            }
-            const uint32_t sum = h[0] + h[1] + h[2] + h[3];
-            uint32_t incl = sum;
-#pragma unroll
-            for (int o = 1; o < WAVE; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, WAVE);
-                if (lane >= o) incl += y;
-            }
-            const uint32_t excl = incl - sum;
-            const unsigned long long bm = __ballot(kk > excl && kk <= incl);
-            const int L = bm ? __ffsll((long long)bm) - 1 : 0;
-            uint32_t bin = 0, below = excl, cnt = 0;
-            if (lane == L) {
-                bool f = false;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (!f && below + h[q] >= kk) {
-                        bin = (uint32_t)(4 * L + q);
-                        cnt = h[q];
-                        f = true;
-                    } else if (!f) {
-                        below += h[q];
-                    }
-                }
-            }
-            bin = __shfl(bin, L, WAVE);
-            below = __shfl(below, L, WAVE);
-            cnt = __shfl(cnt, L, WAVE);
-            kk -= below;
-            prefix |= bin << shift;
-            if (cnt == 1 && pass < 3) {  // the single key with this prefix is the answer
-                const uint32_t nmask = 0xFFFFFFFFu << shift;
-                uint32_t val = 0;
-                bool have = false;
-#pragma unroll
-                for (int j = 0; j < KPL; ++j)
-                    if (!have && (key[j] & nmask) == prefix) {
-                        val = key[j];
-                        have = true;
-                    }
-                const unsigned long long hm = __ballot(have);
-                answer = __shfl(val, __ffsll((long long)hm) - 1, WAVE);
-                found = true;
-                break;
-            }
-            __builtin_amdgcn_wave_barrier();  // the next zeroing after every lane's histogram reads
+#ifdef KTH_ROWS_LEGACY
+        answer = row_select_radix<KPL, R0>(key, hist, lane, kk);
+#else
+        answer = row_select_range<F32, KPL, R0>(key, hist, lane, kk, cols, flip);
+#endif
         }
-        if (!found) answer = prefix;
         if (!TOPK) {
             if (lane == 0) out[r] = raw_of_key<F32>(answer ^ flip);
         } else {

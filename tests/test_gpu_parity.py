@@ -255,6 +255,73 @@ def test_rows_f32(gpu, cols):
         np.testing.assert_array_equal(_f32_order_key(got), _f32_order_key(want), err_msg=f"k={k}")
 
 
+def _f32_adversarial_rows(rng, rows, cols):
+    """Rows that stress the value-linear first pass of the row kernel: huge and
+    tiny value ranges, subnormals, infinities, NaN, signed zeros, a few
+    distinct values, clusters a few ulps wide, and one outlier per row."""
+    m = rng.uniform(-1, 1, size=(rows, cols)).astype(np.float32)
+    fams = [
+        lambda: rng.uniform(-3e38, 3e38, cols),                       # range overflows float
+        lambda: rng.uniform(-1e-38, 1e-38, cols),                     # subnormals / tiny
+        lambda: np.float32(1.0) + rng.integers(0, 8, cols) * np.float32(2 ** -23),  # ulp cluster
+        lambda: np.where(rng.random(cols) < 0.5, np.inf, -np.inf),
+        lambda: np.where(rng.random(cols) < 0.1, np.nan, rng.uniform(-1, 1, cols)),
+        lambda: np.where(rng.random(cols) < 0.5, -0.0, 0.0),
+        lambda: rng.choice(np.array([-2.5, 0.0, 7.0, 1e30], dtype=np.float32), cols),
+        lambda: np.concatenate([rng.normal(0, 1, cols - 1), [1e35]]),  # one outlier
+        lambda: np.concatenate([rng.normal(0, 1, cols - 1), [np.inf]]),
+        lambda: np.exp(rng.normal(0, 10, cols)),                      # log-normal, wide
+        lambda: rng.uniform(-1, 1, cols) * np.float32(1e-30),
+        lambda: np.full(cols, 3.0),
+    ]
+    for i in range(rows):
+        if i % 2 == 0:
+            m[i] = np.asarray(fams[(i // 2) % len(fams)](), dtype=np.float64).astype(np.float32)
+    return m
+
+
+@pytest.mark.parametrize("cols", [4096, 2048, 1000, 333])
+def test_rows_f32_adversarial(gpu, cols):
+    import torch
+    rows = 96
+    rng = np.random.default_rng(cols + 99)
+    with np.errstate(over="ignore", invalid="ignore"):
+        m = _f32_adversarial_rows(rng, rows, cols)
+    d = torch.from_numpy(m).cuda()
+    out = torch.empty(rows, dtype=torch.float32, device="cuda")
+    keys = _f32_order_key(m)
+    for k in sorted({1, 2, 64, cols // 3, cols // 2, cols - 1, cols}):
+        gpu.rows(d, rows, cols, k, out, f32=True)
+        gpu.sync()
+        got = out.cpu().numpy()
+        idx = np.argsort(keys, axis=1, kind="stable")[:, k - 1]
+        want = m[np.arange(rows), idx]
+        np.testing.assert_array_equal(_f32_order_key(got), _f32_order_key(want), err_msg=f"k={k}")
+
+
+@pytest.mark.parametrize("cols", [4096, 1000])
+def test_rows_i32_ranges(gpu, cols):
+    """Row key ranges of every width (the row kernel normalises each row to its
+    own [min, max]): narrow, wide, one outlier, INT_MIN/INT_MAX mixes."""
+    import torch
+    rows = 64
+    rng = np.random.default_rng(cols + 5)
+    m = np.empty((rows, cols), dtype=np.int64)
+    for i in range(rows):
+        w = 1 << (i % 33)
+        lo = int(rng.integers(-2 ** 31, 2 ** 31 - min(w, 2 ** 31 - 1)))
+        m[i] = rng.integers(lo, min(lo + w, 2 ** 31), size=cols) if w > 1 else lo
+        if i % 5 == 0:
+            m[i, int(rng.integers(cols))] = 2 ** 31 - 1 if i % 2 else -2 ** 31
+    m = m.astype(np.int32)
+    d = torch.from_numpy(m).cuda()
+    out = torch.empty(rows, dtype=torch.int32, device="cuda")
+    for k in sorted({1, 2, 64, cols // 2, cols - 1, cols}):
+        gpu.rows(d, rows, cols, k, out)
+        gpu.sync()
+        np.testing.assert_array_equal(out.cpu().numpy(), _row_ref(m, k), err_msg=f"k={k}")
+
+
 # ------------------------------------------------------------- top-k rows
 def _topk_ref(keys, k, largest):
     """Column-order top-k with ties by column: numpy restatement of the contract
@@ -296,6 +363,24 @@ def test_topk_rows_f32(gpu, largest):
     m = rng.uniform(-1, 1, size=(rows, cols)).astype(np.float32)
     m[1] = np.round(m[1] * 4) / 4
     m[2, :6] = [np.nan, -0.0, 0.0, np.inf, -np.inf, np.nan]
+    d = torch.from_numpy(m).cuda()
+    vals = torch.empty((rows, k), dtype=torch.float32, device="cuda")
+    idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+    gpu.topk_rows(d, rows, cols, k, vals, idx, largest=largest, f32=True)
+    gpu.sync()
+    want_idx = _topk_ref(_f32_order_key(m).astype(np.int64), k, largest)
+    np.testing.assert_array_equal(idx.cpu().numpy(), want_idx)
+    got = vals.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, np.take_along_axis(m, want_idx, axis=1).view(np.uint32))
+
+
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_rows_f32_adversarial(gpu, largest):
+    import torch
+    rows, cols, k = 96, 4096, 64
+    rng = np.random.default_rng(17)
+    with np.errstate(over="ignore", invalid="ignore"):
+        m = _f32_adversarial_rows(rng, rows, cols)
     d = torch.from_numpy(m).cuda()
     vals = torch.empty((rows, k), dtype=torch.float32, device="cuda")
     idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
