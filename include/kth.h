@@ -174,6 +174,10 @@ int kth_dist_result(kth_ctx *ctx, int32_t *d_out);
  * per rank (a multiple of 64, at least 64), so that the all-gathered sample
  * has the single-GPU size. */
 int64_t kth_dist_sample_size(int64_t n);
+/* Sampler layout (diagnostics and tests): a sample of s keys from n is read as
+ * ceil(s / C) chunks of C = kth_sample_chunk() consecutive keys, chunk c at
+ * key c * (n / ceil(s / C)); the last chunk holds the remaining s mod C keys. */
+int kth_sample_chunk(void);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,7 @@ constexpr int64_t RADIX_MAX_N = 1ll << 22;   // radix path up to here, window pa
 constexpr int64_t SAMPLE_MAX = 1ll << 20;    // sample keys (single GPU / total over ranks)
 constexpr double WINDOW_Z = 6.0;             // window half-width in sample standard deviations
 constexpr int LEVEL_GRID_MAX = 1024;
+constexpr int POST_DENSE_GRID = 256;  // the candidates need ~100 dense WGs; the rare fallback streams the input with 256
 int gather_grid(u64 nchunks) {
     const u64 per_wg = (u64)(kth::DENSE_BLK / kth::WAVE) * kth::GATHER_BATCH;  // chunks per workgroup round
     return (int)std::max<u64>(1, (nchunks + per_wg - 1) / per_wg);
@@ -58,6 +59,8 @@ struct kth_ctx {
     int device = 0;
     int main_grid = 0;  // streaming-pass workgroups (num_cu * 8; KTH_MAIN_WG_PER_CU overrides)
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
+    int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
+    int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -291,7 +294,7 @@ int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
 // histogram in islot(0).
 int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
     const int64_t s = sample_size(n);
-    const u64 nchunks = (u64)s / kth::SAMPLE_CHUNK;
+    const u64 nchunks = ((u64)s + kth::SAMPLE_CHUNK - 1) / kth::SAMPLE_CHUNK;
     const u64 stride = (u64)n / nchunks;
     u64 r_lo, r_hi;
     window_ranks(n, k, s, &r_lo, &r_hi);
@@ -305,7 +308,8 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.init_s = (u64)s;
     a.r_lo = r_lo;
     a.r_hi = r_hi;
-    kth::k_gather<true><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, keys, stride, c->sample, (u64)s);
+    kth::k_gather<true><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, keys, (u64)n, stride, c->sample,
+                                                                              (u64)s);
     // digits 2, 3 of the sample ranks (sparse: only keys in the picked bins)
     const int gs = level_grid((u64)s, sparse_wg(c));
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), islot(c, 2), islot(c, 0));
@@ -328,15 +332,15 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), islot(c, 2), islot(c, 0));
     a.keys = keys;
     a.n_local = (u64)n;
-    launch_level(c, a, true, LEVEL_GRID_MAX);
+    launch_level(c, a, true, c->post_dense_grid);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 2), islot(c, 0), islot(c, 1));
     a.keys = keys;
     a.n_local = (u64)n;
-    launch_level(c, a, false, LEVEL_GRID_MAX);
+    launch_level(c, a, false, c->post_sparse_grid);
     a = step(c, kth::ADV_PICK, 1, 0, islot(c, 0), islot(c, 1), islot(c, 2));
     a.keys = keys;
     a.n_local = (u64)n;
-    launch_level(c, a, false, LEVEL_GRID_MAX);
+    launch_level(c, a, false, c->post_sparse_grid);
     a = step(c, kth::ADV_PICK, 0, 1, islot(c, 1), nullptr, nullptr);
     kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, d_status, c->islots, ISLOT_WORDS);
     c->last_state = 1;
@@ -486,6 +490,8 @@ int kth_ctx_create(int device, kth_ctx **out) {
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
             if (e && atoi(e) > 0) per = atoi(e);
             if (const char *g = getenv("KTH_SPARSE_PER_WG")) c->sparse_per_wg = (u64)std::max(0, atoi(g));
+            if (const char *g = getenv("KTH_POST_DENSE_GRID")) c->post_dense_grid = std::max(1, atoi(g));
+            if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
             c->main_grid = c->num_cu * per;
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
@@ -730,6 +736,8 @@ int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, in
 // ------------------------------------------------------- sharded protocol
 int64_t kth_dist_sample_size(int64_t n) { return sample_size(n); }
 
+int kth_sample_chunk(void) { return kth::SAMPLE_CHUNK; }
+
 int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;
     KTH_TRY(set_device(c));
@@ -749,7 +757,7 @@ int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
 int kth_dist_sample(kth_ctx *c, const int32_t *d_keys, int64_t n_local, uint32_t *d_sample, int64_t s_local) {
     if (!c || !d_keys || !d_sample || s_local < 64 || s_local % 64 || n_local < s_local) return KTH_EINVAL;
     KTH_TRY(set_device(c));
-    const u64 nchunks = (u64)s_local / kth::SAMPLE_CHUNK;
+    const u64 nchunks = ((u64)s_local + kth::SAMPLE_CHUNK - 1) / kth::SAMPLE_CHUNK;
     const u64 stride = (u64)n_local / nchunks;
     StepArgs a;
     memset(&a, 0, sizeof a);
@@ -757,7 +765,7 @@ int kth_dist_sample(kth_ctx *c, const int32_t *d_keys, int64_t n_local, uint32_t
         a.stats_zero = c->uslots;
         a.zero_words = 3 * (u64)KTH_STATS_WORDS;
     }
-    kth::k_gather<false><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, d_keys, stride, d_sample,
+    kth::k_gather<false><<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, d_keys, (u64)n_local, stride, d_sample,
                                                                                 (u64)s_local);
     KTH_TRY(launch_check());
     if (a.zero_words) c->dist_zero = false;

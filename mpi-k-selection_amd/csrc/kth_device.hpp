@@ -187,4 +187,84 @@ __device__ bool block_pick_vals(const u64 (&h)[PER], u64 k, uint32_t *out_bin, u
     return ok;
 }
 
+
+// ------------------------------------------------------ two-target block pick
+// DPP row shifts / broadcasts: a u64 moves as two dwords and is added with a
+// carry, so the scans need no LDS round trip and no per-lane addresses.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ u64 dpp64(u64 x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROWS, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROWS, 0xF, false);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 wave_incl_scan64(u64 x) {
+    x += dpp64<0x111, 0xF>(x);  // row_shr:1
+    x += dpp64<0x112, 0xF>(x);  // row_shr:2
+    x += dpp64<0x114, 0xF>(x);  // row_shr:4
+    x += dpp64<0x118, 0xF>(x);  // row_shr:8
+    x += dpp64<0x142, 0xA>(x);  // row_bcast:15
+    x += dpp64<0x143, 0xC>(x);  // row_bcast:31
+    return x;
+}
+
+// block_pick_vals for two targets at once (target t's histogram in h[t],
+// thread i owning bins [i*PER, i*PER + PER)): one wave scan per target, both
+// chains interleaved, and two barriers in all.  want[t] = false skips target
+// t (its outputs are then unspecified).  ok[t] false if the histogram holds
+// fewer than k[t] keys.  `scratch` holds 2 * (BLOCK/64) + 6 words.
+template <int BLOCK, int PER>
+__device__ void block_pick2(const u64 (&h0)[PER], const u64 (&h1)[PER], const bool want[2], const u64 k[2],
+                            uint32_t bin[2], u64 below[2], bool ok[2], u64 *scratch) {
+    constexpr int NW = BLOCK / WAVE;
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    u64 sum0 = 0, sum1 = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        sum0 += h0[j];
+        sum1 += h1[j];
+    }
+    const u64 inc0 = wave_incl_scan64(sum0), inc1 = wave_incl_scan64(sum1);
+    u64 *wsum = scratch, *res = scratch + 2 * NW;
+    if (lane == WAVE - 1) {
+        wsum[wid] = inc0;
+        wsum[NW + wid] = inc1;
+    }
+    if (threadIdx.x < 6) res[threadIdx.x] = 0;
+    __syncthreads();
+    u64 pre0 = inc0 - sum0, pre1 = inc1 - sum1;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+        if (w < wid) {
+            pre0 += wsum[w];
+            pre1 += wsum[NW + w];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const u64 kt = k[t], pre = t ? pre1 : pre0, sum = t ? sum1 : sum0;
+        if (want[t] && kt >= 1 && kt > pre && kt <= pre + sum) {  // exactly one thread
+            u64 cum = pre;
+            bool found = false;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const u64 hj = t ? h1[j] : h0[j];
+                if (!found && cum + hj >= kt) {
+                    res[3 * t + 0] = 1;
+                    res[3 * t + 1] = (u64)(threadIdx.x * PER + j);
+                    res[3 * t + 2] = cum;
+                    found = true;
+                }
+                cum += hj;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        ok[t] = res[3 * t] != 0;
+        bin[t] = (uint32_t)res[3 * t + 1];
+        below[t] = res[3 * t + 2];
+    }
+}
+
 }  // namespace kth

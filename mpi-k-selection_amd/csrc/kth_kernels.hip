@@ -35,11 +35,11 @@ constexpr int WREG = KTH_WREG;        // per-wave candidate staging region (word
 constexpr int LEVEL_UNROLL = 8;       // 16-B loads in flight per thread in k_level
 constexpr int DENSE_BLK = 1024;       // workgroup size of the dense-histogram levels
 #ifndef KTH_SAMPLE_CK
-#define KTH_SAMPLE_CK 1
+#define KTH_SAMPLE_CK 16
 #endif
-constexpr int SAMPLE_CK = KTH_SAMPLE_CK;            // sampled keys per lane per chunk (1 or 4)
+constexpr int SAMPLE_CK = KTH_SAMPLE_CK;            // sampled keys per lane per chunk (1, 4, 16, 64)
 constexpr int SAMPLE_CHUNK = WAVE * SAMPLE_CK;      // keys per sampled chunk = one wave's load
-constexpr int GATHER_BATCH = 16 / SAMPLE_CK;        // sampled chunks in flight per wave
+constexpr int GATHER_BATCH = SAMPLE_CK < 16 ? 16 / SAMPLE_CK : 1;  // sampled chunks in flight per wave
 constexpr int SMALL_BLOCK = 1024;
 constexpr int ROWS_BLOCK = 256;
 
@@ -178,29 +178,37 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
         if (threadIdx.x == 0 && ss.mode == MODE_MAIN) decide(ss, a.stats_in);
         __syncthreads();
     } else if (a.adv == ADV_PICK) {
+        // both targets' digits in one pass (two barriers); target 1 reads
+        // target 0's histogram when they share a prefix
+        const uint32_t mode = ss.mode;
+        const bool live = mode == MODE_SAMPLE || mode == MODE_CAND || mode == MODE_FULL;
+        bool want[2];
+        u64 kt[2];
+#pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const uint32_t mode = ss.mode;
-            const bool need = (mode == MODE_SAMPLE || mode == MODE_CAND || mode == MODE_FULL) &&
-                              ss.t[t].active && ss.t[t].done < ss.W;
-            if (!need) continue;  // block-uniform: read from LDS after a barrier
-            const uint32_t d = digit_bits(ss.W, ss.t[t].done);
-            const bool use0 = t == 0 || ss.share;
-            uint32_t bin;
-            u64 below;
-            const bool ok = block_pick_vals<BLOCK, PER>(use0 ? h0 : h1, ss.t[t].k, &bin, &below, scratch);
-            if (threadIdx.x == 0) {
-                if (!ok || bin >= (1u << d)) {
+            want[t] = live && ss.t[t].active && ss.t[t].done < ss.W;
+            kt[t] = ss.t[t].k;
+        }
+        const bool share = ss.share;
+        uint32_t bin[2];
+        u64 below[2];
+        bool ok[2];
+        if (want[0] || want[1]) block_pick2<BLOCK, PER>(h0, share ? h0 : h1, want, kt, bin, below, ok, scratch);
+        if (threadIdx.x == 0) {
+            for (int t = 0; t < 2; ++t) {
+                if (!want[t] || ss.mode == MODE_DONE) continue;
+                const uint32_t d = digit_bits(ss.W, ss.t[t].done);
+                if (!ok[t] || bin[t] >= (1u << d)) {
                     ss.error = 1 + t;
                     ss.mode = MODE_DONE;
                 } else {
-                    ss.t[t].k -= below;
-                    ss.t[t].prefix = (ss.t[t].prefix << d) | bin;
+                    ss.t[t].k -= below[t];
+                    ss.t[t].prefix = (ss.t[t].prefix << d) | bin[t];
                     ss.t[t].done += d;
                 }
             }
-            __syncthreads();
+            resolve(ss);
         }
-        if (threadIdx.x == 0) resolve(ss);
         __syncthreads();
     }
 }
@@ -333,9 +341,11 @@ __device__ __forceinline__ void publish(const SelState &ss, uint32_t share, cons
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     __shared__ SelState ss;
-    __shared__ u64 scratch[BLOCK / WAVE + 4];
-    __shared__ uint32_t lh[2][NBINS];
+    __shared__ u64 scratch[2 * (BLOCK / WAVE) + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
     KTH_STAMP(a, 0);
+    // zero the histogram while the advance's loads are in flight (its barrier orders it)
+    for (int i = threadIdx.x; i < 2 * NBINS / 4; i += BLOCK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
     advance<BLOCK>(ss, a, scratch);
     KTH_STAMP(a, 1);
     bool share;
@@ -354,8 +364,6 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     const u64 want = (count + a.min_per_wg - 1) / a.min_per_wg;
     const uint32_t active = (uint32_t)min((u64)gridDim.x, want);
     if (blockIdx.x >= active) return;
-    for (int i = threadIdx.x; i < 2 * NBINS; i += BLOCK) (&lh[0][0])[i] = 0;
-    __syncthreads();
     KTH_STAMP(a, 2);
     auto f = [&](const uint32_t *k, uint32_t valid, auto full) {
 #pragma unroll
@@ -377,11 +385,11 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
 // shard (stride = chunk distance in keys).  With FUSE the first digit's
 // histogram of the sample is built too (single-GPU: the sample is complete).
 template <bool FUSE>
-__global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 stride,
-                                                uint32_t *__restrict__ sample, u64 s) {
+__global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 n_keys,
+                                                u64 stride, uint32_t *__restrict__ sample, u64 s) {
     __shared__ SelState ss;
-    __shared__ u64 scratch[DENSE_BLK / WAVE + 4];
-    __shared__ uint32_t lh[2][NBINS];
+    __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
     HistPlan plan;
     bool share = false;
     KTH_STAMP(a, 0);
@@ -397,25 +405,40 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
             a.stats_zero[i] = 0;
     }
     const int lane = threadIdx.x & (WAVE - 1);
-    const u64 nchunks = s / SAMPLE_CHUNK;
+    // chunks of SAMPLE_CHUNK keys at `stride`; the last one holds s % SAMPLE_CHUNK
+    // keys when that is nonzero (scalar loads, guarded by s and n_keys)
+    const u64 nfull = s / SAMPLE_CHUNK, nchunks = (s + SAMPLE_CHUNK - 1) / SAMPLE_CHUNK;
     const u64 gw = ((u64)blockIdx.x * DENSE_BLK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (DENSE_BLK / WAVE);
     // every wave owns GATHER_BATCH consecutive chunk slots per round; all loads
-    // of a round are in flight together (the chunks are 256 KiB apart in HBM)
-    const bool vec = SAMPLE_CK == 4 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0 && stride % 4 == 0;
+    // of a round are in flight together.  Chunks of >= 256 keys are read as
+    // 16-byte loads, q-th load of the wave = 1 KiB contiguous (lane-major).
+    const bool vec = SAMPLE_CK >= 4 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0 && stride % 4 == 0;
+    constexpr int NV = SAMPLE_CK >= 4 ? SAMPLE_CK / 4 : 1;  // 16-byte loads per lane per chunk
+    auto off_of = [&](int q) -> u64 {  // key q of this lane within its chunk
+        return SAMPLE_CK >= 4 ? 4 * ((u64)(q / 4) * WAVE + lane) + (q & 3) : (u64)lane;
+    };
     for (u64 c0 = gw * GATHER_BATCH; c0 < nchunks; c0 += nw * GATHER_BATCH) {
         uint32_t kk[GATHER_BATCH][SAMPLE_CK];
 #pragma unroll
         for (int j = 0; j < GATHER_BATCH; ++j) {
             const u64 c = c0 + j;
-            const int32_t *src = keys + c * stride + lane * SAMPLE_CK;
-            if (SAMPLE_CK == 4 && vec) {
-                const uint4 x = c < nchunks ? *reinterpret_cast<const uint4 *>(src) : make_uint4(0, 0, 0, 0);
-                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+            if (SAMPLE_CK >= 4 && vec && c < nfull) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
 #pragma unroll
-                for (int q = 0; q < SAMPLE_CK; ++q) kk[j][q] = key_of_i32(xs[q & 3]);
+                for (int q = 0; q < NV; ++q) {
+                    const uint4 x = src[q * WAVE + lane];
+                    kk[j][4 * q + 0] = key_of_i32(x.x);
+                    kk[j][4 * q + 1] = key_of_i32(x.y);
+                    kk[j][4 * q + 2] = key_of_i32(x.z);
+                    kk[j][4 * q + 3] = key_of_i32(x.w);
+                }
             } else {
 #pragma unroll
-                for (int q = 0; q < SAMPLE_CK; ++q) kk[j][q] = c < nchunks ? key_of_i32((uint32_t)src[q]) : 0u;
+                for (int q = 0; q < SAMPLE_CK; ++q) {
+                    const u64 off = off_of(q);
+                    const bool ok = c < nchunks && c * SAMPLE_CHUNK + off < s && c * stride + off < n_keys;
+                    kk[j][q] = ok ? key_of_i32((uint32_t)keys[c * stride + off]) : 0u;
+                }
             }
         }
 #pragma unroll
@@ -424,8 +447,11 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
             if (c < nchunks) {
 #pragma unroll
                 for (int q = 0; q < SAMPLE_CK; ++q) {
-                    sample[c * SAMPLE_CHUNK + lane * SAMPLE_CK + q] = kk[j][q];
-                    if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j][q], true);
+                    const u64 off = off_of(q);
+                    if (c * SAMPLE_CHUNK + off < s) {
+                        sample[c * SAMPLE_CHUNK + off] = kk[j][q];
+                        if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j][q], true);
+                    }
                 }
             }
         }
@@ -526,7 +552,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     constexpr int U = MAIN_UNROLL, S = MAIN_SUB, K = 4 * S;
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
-    __shared__ u64 scratch[BLK / WAVE + 4];
+    __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
     __shared__ uint32_t region[BLK / WAVE][WREG];
     __shared__ u64 red[6][BLK / WAVE];
     KTH_STAMP(a, 0);
@@ -644,7 +670,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
 __global__ __launch_bounds__(BLK) void k_result(StepArgs a, int32_t *d_out, int32_t *d_status, u64 *izero,
                                                 u64 izero_words) {
     __shared__ SelState ss;
-    __shared__ u64 scratch[BLK / WAVE + 4];
+    __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
     KTH_STAMP(a, 0);
     advance<BLK>(ss, a, scratch);
     if (threadIdx.x == 0) {

@@ -101,6 +101,7 @@ PROTOS = {
     "kth_dist_level": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int]),
     "kth_dist_result": (ctypes.c_int, [c_vp, c_vp]),
     "kth_dist_sample_size": (ctypes.c_int64, [ctypes.c_int64]),
+    "kth_sample_chunk": (ctypes.c_int, []),
     # vector.h
     "VecNew": (IntVectorPtr, [ctypes.c_int]),
     "VecAdd": (ctypes.c_int, [IntVectorPtr, ctypes.c_int]),

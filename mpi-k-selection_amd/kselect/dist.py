@@ -6,7 +6,7 @@ Replaces the CGM driver of the reference (TODO-kth-problem-cgm.c:76-278):
   -------------------------------------          -----------------------------------
   :103 MPI_Scatterv of 4n bytes from rank 0      shards already resident per GPU
   :115 local qsort (88% of CGM time)             --
-  :125-131 local median                          local sample (64-key chunks)
+  :125-131 local median                          local sample (chunks of kth_sample_chunk() keys)
   :135-136 2x MPI_Gather (median, n_i)           all_gather of the samples
   :139-165 weighted median on rank 0             every rank derives the same window
   :168 MPI_Bcast of the pivot                    -- (deterministic, no broadcast)

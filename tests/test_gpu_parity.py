@@ -134,10 +134,15 @@ def test_window_fallback_is_exact(gpu):
     n = 1 << 24
     keys = _dev_keys(gpu, n, "uniform_full")
     fresh = kselect.Selector(0)  # candidate capacity sized for this n (the shared ctx grew for 2^30)
-    # k_gather samples chunks of 64 keys at stride n / (s/64); overwrite those chunks
-    s = min(1 << 20, (n // 64) & ~63)
-    stride = n // (s // 64)
-    idx = (torch.arange(s // 64, device="cuda") * stride).repeat_interleave(64) + torch.arange(64, device="cuda").repeat(s // 64)
+    # k_gather samples ceil(s/C) chunks of C keys at stride n / ceil(s/C)
+    # (include/kth.h kth_sample_chunk); overwrite those chunks
+    from kselect._lib import load
+    lib = load()
+    s = int(lib.kth_dist_sample_size(n))
+    c = int(lib.kth_sample_chunk())
+    nch = -(-s // c)
+    stride = n // nch
+    idx = (torch.arange(nch, device="cuda") * stride).repeat_interleave(c) + torch.arange(c, device="cuda").repeat(nch)
     keys[idx] = 5
     srt = np.sort(keys.cpu().numpy())
     for k in (1, n // 2, n):
