@@ -51,7 +51,7 @@ struct Target {
     uint32_t pad;
 };
 
-struct SelState {
+struct alignas(16) SelState {
     u64 n, k;          // global input size and rank
     u64 s;             // sample size (window phase)
     u64 cnt[5];        // reduced streaming-pass counts (lt, eq_lo, eq_hi, inside, ovf)

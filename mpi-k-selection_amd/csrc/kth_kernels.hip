@@ -73,11 +73,20 @@ struct StepArgs {
 
 // Diagnostic phase stamps (KTH_STAMPS=1 only; null pointer in the product):
 // thread 0 of each workgroup records the 100 MHz wall clock at point i.
+// Compiled in only with -DKTH_STAMPS_BUILD (tools' diagnostic variant): the
+// runtime null check alone made every kernel wait for that kernel argument
+// before issuing its first loads.
+#ifdef KTH_STAMPS_BUILD
 #define KTH_STAMP(a, i)                                                                          \
     do {                                                                                         \
         if ((a).stamps && threadIdx.x == 0)                                                      \
             (a).stamps[(u64)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();           \
     } while (0)
+#else
+#define KTH_STAMP(a, i) \
+    do {                \
+    } while (0)
+#endif
 
 // ------------------------------------------------------------- the advance
 __device__ __forceinline__ void resolve(SelState &s) {
@@ -137,6 +146,14 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
     // state: a digit has at most NBINS bins and bins past 2^d are zero in a
     // zeroed slot, so picking over all NBINS is exact for any digit width.
     constexpr int PER = NBINS / BLOCK;
+    constexpr int SV = sizeof(SelState) / 16;
+    static_assert(sizeof(SelState) % 16 == 0 && SV <= BLOCK, "state moves as 16-byte words");
+    // The previous kernel's state, loaded by the first SV threads as 16-byte
+    // words before anything else, so its latency overlaps the histogram's
+    // (thread 0 loading it after the histogram serialised two HBM round trips).
+    const bool carry = a.adv != ADV_INIT_SAMPLE && a.adv != ADV_INIT_FULL;
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    if (carry && threadIdx.x < SV) sv = reinterpret_cast<const uint4 *>(a.st_in)[threadIdx.x];
     u64 h0[PER], h1[PER];
     if (a.adv == ADV_PICK) {
         const u64 *b0 = a.stats_in + NCOUNTS + threadIdx.x * PER;
@@ -169,10 +186,9 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
                 s.t[0] = Target{a.init_k, 0, 0, 1, 0};
             }
             ss = s;
-        } else {
-            ss = *a.st_in;
         }
     }
+    if (carry && threadIdx.x < SV) reinterpret_cast<uint4 *>(&ss)[threadIdx.x] = sv;
     __syncthreads();
     if (a.adv == ADV_DECIDE) {
         if (threadIdx.x == 0 && ss.mode == MODE_MAIN) decide(ss, a.stats_in);
