@@ -197,6 +197,13 @@ def rows_main(args):
     keys_total = R * C * world
     value = keys_total / (elapsed / args.steps) / 1e9
     achieved = 4.0 * R * C / (kern_ms * 1e-3) / 1e9
+    rows_traffic = None  # PMC HBM bytes per launch (tools/gpu_profiles.sh), for this exact workload
+    tpath = os.path.join(REPO, "profiles", f"pmc_traffic_rows_{args.rows_dtype}.json")
+    if os.path.exists(tpath) and not args.topk and (R, C, k) == (65536, 4096, 64):
+        try:
+            rows_traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            rows_traffic = None
     res = {
         "metric": ("Gkeys/s batched top-k (largest) per row" if args.topk else "Gkeys/s batched k-th per row")
                   + " (65536 x 4096, BASELINE config 5)",
@@ -207,8 +214,9 @@ def rows_main(args):
         "config": {"workload": f"{'top-k' if args.topk else 'k-th'} per row of a {R} x {C} "
                                f"{'f32' if f32 else 'int32'} matrix, k={k}",
                    "rows": R, "cols": C, "k": k, "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "kth::k_rows", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": "kth::k_rows_reg" if C <= 4096 else "kth::k_rows",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": rows_traffic,
                      "algorithmic_bytes_per_launch": 4 * R * C, "avg_launch_ms": kern_ms},
         "verified": verified,
     }
