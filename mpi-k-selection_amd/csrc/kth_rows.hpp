@@ -21,6 +21,10 @@
 namespace kth {
 
 constexpr int RW_BLOCK = 256;
+#ifndef KTH_TOPK_RELOAD
+#define KTH_TOPK_RELOAD 1
+#endif
+constexpr bool TOPK_RELOAD = KTH_TOPK_RELOAD;  // top-k compaction re-reads full rows from L2
 #ifndef KTH_ROWS_WAVES
 #define KTH_ROWS_WAVES 4  // waves per SIMD the register budget is held to (<= 128 VGPRs)
 #endif
@@ -471,7 +475,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
 // order reversed: ~key).
 // FULL: cols == 64 * KPL and 16-byte aligned rows (unguarded loads, row_select_fast).
 template <bool F32, int KPL, bool VEC, int R0, bool TOPK, bool FULL>
-__global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
+__global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL)) ? 2 : KTH_ROWS_WAVES) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
                                                       uint32_t k, uint32_t *__restrict__ out, uint32_t flip,
                                                       uint32_t *__restrict__ vals, int32_t *__restrict__ idx) {
     static_assert(KPL % 4 == 0, "16-byte loads");
@@ -486,7 +490,9 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) voi
         if (FULL) {
 #pragma unroll
             for (int j = 0; j < KPL / 4; ++j) {
-                const uint4 x = load_nt(reinterpret_cast<const uint4 *>(row + (j * WAVE + lane) * 4));
+                // top-k re-reads the row for its compaction: keep it in L2 (no non-temporal hint)
+                const uint4 *src = reinterpret_cast<const uint4 *>(row + (j * WAVE + lane) * 4);
+                const uint4 x = TOPK_RELOAD && TOPK ? *src : load_nt(src);
                 key[4 * j + 0] = x.x;
                 key[4 * j + 1] = x.y;
                 key[4 * j + 2] = x.z;
@@ -544,16 +550,15 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) voi
             auto below_lane = [](unsigned long long b) {  // set bits of b in lanes below this one
                 return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             };
-#pragma unroll
-            for (int j = 0; j < KPL / 4; ++j) {
-                const uint32_t e = (uint32_t)(j * WAVE + lane) * 4u;
+            // One group of 4 keys (columns e .. e + 3) of this lane.
+            auto group = [&](uint32_t e, const uint32_t (&g)[4]) __attribute__((always_inline)) {
                 bool lt[4], eq[4], sel[4];
                 uint32_t eq_below = 0, eq_tot = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const bool valid = e + q < cols;
-                    lt[q] = valid && key[4 * j + q] < answer;
-                    eq[q] = valid && key[4 * j + q] == answer;
+                    const bool valid = FULL || e + q < cols;
+                    lt[q] = valid && g[q] < answer;
+                    eq[q] = valid && g[q] == answer;
                     const unsigned long long be = __ballot(eq[q]);
                     eq_below += below_lane(be);
                     eq_tot += (uint32_t)__popcll(be);
@@ -571,7 +576,7 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) voi
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (sel[q]) {
-                        const uint32_t x = raw_of_key<F32>(key[4 * j + q] ^ flip);
+                        const uint32_t x = raw_of_key<F32>(g[q] ^ flip);
                         if (stage) {  // the histogram is free now: stage (value, column) pairs
                             hist[2 * pos] = x;
                             hist[2 * pos + 1] = e + q;
@@ -583,7 +588,32 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : TOPK ? 2 : KTH_ROWS_WAVES) voi
                     }
                 taken += tot;
                 eq_seen += eq_tot;
-                __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+            };
+            if (TOPK_RELOAD && FULL) {
+                // FULL rows re-read their keys here (from L2: loaded without the
+                // non-temporal hint), two groups ahead, in a rolled loop, instead of
+                // keeping all KPL keys live through the compaction: 4 waves per
+                // SIMD instead of 2.
+                const uint4 *src = reinterpret_cast<const uint4 *>(row);
+                uint4 nx = src[lane], nx2 = src[WAVE + lane];  // two groups in flight
+#pragma unroll 1
+                for (int j = 0; j < KPL / 4; ++j) {
+                    const uint4 x = nx;
+                    nx = nx2;
+                    if (j + 2 < KPL / 4) nx2 = src[(j + 2) * WAVE + lane];
+                    const uint32_t raw[4] = {x.x, x.y, x.z, x.w};
+                    uint32_t g[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) g[q] = (F32 ? key_of_f32(raw[q]) : key_of_i32(raw[q])) ^ flip;
+                    group((uint32_t)(j * WAVE + lane) * 4u, g);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPL / 4; ++j) {
+                    const uint32_t g[4] = {key[4 * j], key[4 * j + 1], key[4 * j + 2], key[4 * j + 3]};
+                    group((uint32_t)(j * WAVE + lane) * 4u, g);
+                    __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+                }
             }
             if (stage) {  // coalesced copy-out of the staged pairs
                 __builtin_amdgcn_wave_barrier();
