@@ -93,6 +93,43 @@ def test_paths_vs_oracle(gpu, oracle, n):
             assert got == srt[k - 1], (fam, n, k, got, srt[k - 1], gpu.stats())
 
 
+def _fuzz_keys(rng, n, kind):
+    """Distributions the synthetic families do not cover: they move the window
+    and the candidate set around (not uniform, clustered, spiky, narrow)."""
+    if kind == "normal":
+        a = rng.normal(0, 2e8, n)
+    elif kind == "exponential":
+        a = rng.exponential(1e6, n) - 5e5
+    elif kind == "narrow":  # heavy duplicates: 4096 distinct values
+        a = rng.integers(-2048, 2048, n)
+    elif kind == "spike_median":  # 30 % of the keys on one value near the median
+        a = rng.integers(-2 ** 31, 2 ** 31, n)
+        a[rng.random(n) < 0.3] = 12345
+    elif kind == "clusters":  # 5 tight clusters
+        c = rng.integers(-2 ** 30, 2 ** 30, 5)
+        a = c[rng.integers(0, 5, n)] + rng.integers(-1000, 1000, n)
+    elif kind == "two_values":
+        a = np.where(rng.random(n) < 0.5, -7, 2 ** 31 - 1)
+    else:  # "blocks": sorted runs, each run from its own range
+        a = np.sort(rng.integers(-2 ** 31, 2 ** 31, n).reshape(-1, n // 8), axis=1).reshape(-1)
+    return np.clip(a, -2 ** 31, 2 ** 31 - 1).astype(np.int32)
+
+
+@pytest.mark.parametrize("kind", ["normal", "exponential", "narrow", "spike_median", "clusters", "two_values",
+                                  "blocks"])
+def test_window_path_fuzz(gpu, kind):
+    """Window path (n > 4 Mi, including sample sizes that end in a partial chunk)
+    on non-uniform inputs, random k: GPU == np.partition."""
+    import torch
+    rng = np.random.default_rng(sum(map(ord, kind)))  # stable across processes
+    for n in (5_000_008, (1 << 23) + 4096):
+        a = _fuzz_keys(rng, n, kind)
+        d = torch.from_numpy(a).cuda()
+        for k in sorted({1, n, n // 2, int(rng.integers(1, n + 1)), int(rng.integers(1, n + 1))}):
+            want = np.partition(a, k - 1)[k - 1]
+            assert gpu.select(d, k) == want, (kind, n, k, gpu.stats())
+
+
 def test_unaligned_device_pointer(gpu):
     """Shards start anywhere: 4-byte but not 16-byte aligned inputs."""
     import torch
