@@ -347,8 +347,8 @@ __device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
 // Fast path for full rows (cols = 64 * KPL, 16-byte aligned): one histogram
 // pass, then the keys of the picked bin go to an LDS list and are ranked there.
 //   pass A: 256 bins of a monotone map b(x) -- the top byte of the order key
-//       (int32, and float rows holding a NaN or an infinity), or for finite
-//       float rows a bin LINEAR IN THE VALUE over the row's own [vmin, vmax]
+//       (int32, and float rows holding a NaN), or for NaN-free float rows a
+//       bin LINEAR IN THE VALUE over (about) the row's own [vmin, vmax]
 //       (vbin), so uniform floats fill the bins evenly instead of piling onto
 //       a few exponent bytes.  Float keys stay raw bits until they are needed
 //       as order keys;
@@ -375,16 +375,23 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     bool fmap = false;
     float fs = 0.f, fo = 0.f;
     if (F32) {  // key[] holds raw float bits
+        // The bin map's range comes from every 4th key: keys outside it clamp
+        // into the end bins, which stays monotone (and exact), so the range only
+        // has to be close.  Infinities clamp the same way.  NaNs (last in the
+        // order) would not, so every key is checked for one.
         float vmin = __uint_as_float(key[0]), vmax = vmin;
-        uint32_t amax = 0;  // largest |bits| << 1: > 0xFF000000 iff a NaN, == iff an infinity
+        bool nan = false;
 #pragma unroll
-        for (int j = 0; j < KPL; j += 2) {
-            const float a = __uint_as_float(key[j]), b = __uint_as_float(key[j + 1]);
-            vmin = min3f(vmin, a, b);
-            vmax = max3f(vmax, a, b);
-            amax = max(amax, max(key[j] << 1, key[j + 1] << 1));
+        for (int j = 0; j < KPL; ++j) {
+            const float a = __uint_as_float(key[j]);
+            nan |= a != a;
+            if (j % 8 == 4) {
+                const float b = __uint_as_float(key[j - 4]);
+                vmin = min3f(vmin, a, b);
+                vmax = max3f(vmax, a, b);
+            }
         }
-        amax = wave_max_u32(amax);
+        const bool anynan = __ballot(nan) != 0;
         vmin = __uint_as_float(wave_reduce(__float_as_uint(vmin), 0x7F800000u, [](uint32_t a, uint32_t b) {
             return __float_as_uint(min3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
         }));
@@ -392,8 +399,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             return __float_as_uint(max3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
         }));
         const float range = vmax - vmin, scale = 256.0f / range;
-        fmap = amax < 0xFF000000u && __builtin_isfinite(range) && range > 0.f && __builtin_isfinite(scale) &&
-               scale > 0.f;
+        fmap = !anynan && __builtin_isfinite(range) && range > 0.f && __builtin_isfinite(scale) && scale > 0.f;
         // bins ascend with the selection order: ascending v (flip = 0) or descending
         fs = flip ? -scale : scale;
         fo = flip ? vmax * scale : -vmin * scale;
@@ -426,7 +432,9 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     // vbin(v) == B  <=>  B <= t < B + 1 for t = fma(v, s, o) (the clamp only
     // merges t < 0 into bin 0 and t >= 255 into bin 255): one fma, two compares
     const float s2 = opaque(fs), o2 = opaque(fo);  // recompute t, do not keep the bins
-    const float tlo = bin ? (float)bin : -__builtin_inff(), thi = bin < 255u ? (float)(bin + 1) : __builtin_inff();
+    // (bin 0 takes t = -inf, bin 255 takes t = +inf: infinities clamp there and
+    // t >= NaN is false)
+    const float tlo = bin ? (float)bin : -__builtin_inff(), thi = bin < 255u ? (float)(bin + 1) : __builtin_nanf("");
     const uint32_t lo = opaque(bin << 24);  // top-byte bin B = keys [B << 24, +2^24)
     uint32_t fill = 0;
 #pragma unroll
@@ -434,7 +442,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
         bool in;
         if (vmap) {
             const float t = __builtin_fmaf(__uint_as_float(key[j]), s2, o2);
-            in = t >= tlo && t < thi;
+            in = t >= tlo && !(t >= thi);
         } else {
             in = key[j] - lo <= 0x00FFFFFFu;
         }
