@@ -27,7 +27,16 @@ namespace {
 constexpr int64_t SMALL_N = 16384;           // LDS path
 constexpr int64_t RADIX_MAX_N = 1ll << 22;   // radix path up to here, window path above
 constexpr int64_t SAMPLE_MAX = 1ll << 20;    // sample keys (single GPU / total over ranks)
-constexpr double WINDOW_Z = 6.0;             // window half-width in sample standard deviations
+constexpr double WINDOW_Z = 5.0;             // window half-width in sample standard deviations (two-sided miss 5.7e-7)
+// KTH_WINDOW_Z overrides it (design exploration); read once
+double window_z() {
+    static const double z = [] {
+        const char *e = getenv("KTH_WINDOW_Z");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0.0 ? v : WINDOW_Z;
+    }();
+    return z;
+}
 constexpr int LEVEL_GRID_MAX = 1024;
 constexpr int POST_DENSE_GRID = 256;  // the candidates need ~100 dense WGs; the rare fallback streams the input with 256
 int gather_grid(u64 nchunks) {
@@ -134,7 +143,8 @@ void window_ranks(int64_t n, int64_t k, int64_t s, u64 *r_lo, u64 *r_hi) {
     const double p = (double)k / (double)n;
     const double r = p * (double)s;
     const double sig = std::sqrt(std::max(1.0, (double)s * p * (1.0 - p)));
-    const double lo = std::floor(r - WINDOW_Z * sig - 2.0), hi = std::ceil(r + WINDOW_Z * sig + 2.0);
+    const double z = window_z();
+    const double lo = std::floor(r - z * sig - 2.0), hi = std::ceil(r + z * sig + 2.0);
     *r_lo = lo < 1.0 ? 0 : (u64)lo;                       // 0 = no lower bound
     *r_hi = hi > (double)s ? (u64)s + 1 : (u64)std::max(1.0, hi);  // s+1 = no upper bound
 }
