@@ -227,6 +227,76 @@ def rows_main(args):
     return 0 if verified else 1
 
 
+def topk_main(args):
+    """top-k (k smallest, int64 indices, index order) of one
+    2^log2n int32 array (kth_topk_i32 = select + count pass + ordered
+    compaction); one step = one call.  N > 1: independent replicas."""
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    import kselect
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    sel = kselect.Selector(local_rank, stream=stream)
+    n = 1 << args.log2n
+    k = args.k or 1024
+    keys = torch.empty(n, dtype=torch.int32, device=dev)
+    sel.fill(keys, n, args.family, seed=args.seed + rank, param=7)
+    sel.reserve(n)
+    vals = torch.empty(k, dtype=torch.int32, device=dev)
+    idx = torch.empty(k, dtype=torch.int64, device=dev)
+    for _ in range(args.warmup):
+        sel.topk(keys, n, k, vals, idx)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[2 * i].record(stream)
+        sel.topk(keys, n, k, vals, idx)
+        evs[2 * i + 1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    call_ms = sum(evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(args.steps)) / args.steps
+    # exact check: same values as torch.topk (smallest), indices point at them, index order
+    want = torch.sort(torch.topk(keys, k, largest=False).values).values
+    verified = bool(torch.equal(torch.sort(vals).values, want) and torch.equal(keys[idx], vals)
+                    and bool((idx[1:] > idx[:-1]).all()))
+    achieved = 4.0 * n / (call_ms * 1e-3) / 1e9
+    res = {
+        "metric": "Gkeys/s top-k (smallest, values + int64 indices) of one int32 array",
+        "value": n * world / (elapsed / args.steps) / 1e9, "unit": "Gkeys/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (device counter-based generator, splitmix64)",
+        "config": {"workload": f"top-{k} of 2^{args.log2n} int32 keys, {args.family}", "n": n, "k": k,
+                   "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "whole kth_topk_i32 call (select + k_topk_count + scan + write)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "algorithmic_bytes_per_launch": 4 * n, "avg_launch_ms": call_ms},
+        "verified": verified,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if verified else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -240,8 +310,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="run the sharded (kth_dist_* + RCCL) protocol even on one GPU")
-    ap.add_argument("--workload", choices=["select", "rows"], default="select",
-                    help="select: BASELINE config 2/3 (the metric); rows: config 5, batched k-th per row")
+    ap.add_argument("--workload", choices=["select", "rows", "topk"], default="select",
+                    help="select: BASELINE config 2/3 (the metric); rows: config 5, batched k-th per row; "
+                         "topk: top-k of one array (--k, default 1024)")
     ap.add_argument("--rows", type=int, default=65536)
     ap.add_argument("--cols", type=int, default=4096)
     ap.add_argument("--rows-dtype", choices=["i32", "f32"], default="i32")
@@ -249,6 +320,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "rows":
         return rows_main(args)
+    if args.workload == "topk":
+        return topk_main(args)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))

@@ -128,6 +128,19 @@ int kth_topk_rows_i32(kth_ctx *ctx, const int32_t *d_keys, int64_t rows, int32_t
 int kth_topk_rows_f32(kth_ctx *ctx, const float *d_keys, int64_t rows, int32_t cols, int32_t k, int largest,
                       float *d_vals, int32_t *d_idx);
 
+/* --- top-k of one array ------------------------------------
+ * The k smallest keys of d_keys[0..n) (largest != 0: the k largest) with their
+ * int64 indices, in index order; of the keys equal to the k-th, the first ones
+ * by index.  The reference implies this as sort(a)[0..k) after its select
+ * block (kth-problem-seq.c:32-33, VecQuickSort then index); here it is the
+ * select (kth_select_i32_async) plus a count pass, a chunk scan and an ordered
+ * compaction that reads only the chunks holding output keys.  d_vals: k int32,
+ * d_idx: k int64; either may be NULL (not both).  1 <= k <= n.  Asynchronous on
+ * the ctx stream (device memory only); a device-side inconsistency leaves the
+ * outputs unwritten and shows as kth_ctx_last_stats().error. */
+int kth_topk_i32(kth_ctx *ctx, const int32_t *d_keys, int64_t n, int64_t k, int largest, int32_t *d_vals,
+                 int64_t *d_idx);
+
 /* --- synthetic inputs (bench / tests) --------------------------------------
  * Fills d_out[0..n) with the keys of global indices offset..offset+n of an
  * n_total-key input of family `dist` (oracle/kth_oracle.h enum ko_dist;

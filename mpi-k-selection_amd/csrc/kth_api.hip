@@ -17,6 +17,7 @@
 
 #include "kth.h"
 #include "kth_kernels.hip"
+#include "kth_topk.hpp"
 
 using kth::SelState;
 using kth::StepArgs;
@@ -81,6 +82,8 @@ struct kth_ctx {
     u64 cand_cap = 0;
     int32_t *staging = nullptr;
     u64 staging_cap = 0;
+    u64 *topk = nullptr;  // top-k chunk counts, bases, [need, error]
+    u64 topk_cap = 0;
     int32_t *d_status = nullptr;  // [answer, error]
     int32_t *h_status = nullptr;  // pinned
     SelState *h_state = nullptr;  // pinned
@@ -547,6 +550,7 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->sample) (void)hipFree(c->sample);
     if (c->cand) (void)hipFree(c->cand);
     if (c->staging) (void)hipFree(c->staging);
+    if (c->topk) (void)hipFree(c->topk);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -726,6 +730,41 @@ int kth_topk_rows_f32(kth_ctx *c, const float *d_keys, int64_t rows, int32_t col
     KTH_TRY(set_device(c));
     return launch_rows<true, true>(c, reinterpret_cast<const uint32_t *>(d_keys), rows, cols, k, nullptr,
                                    largest ? 0xFFFFFFFFu : 0u, reinterpret_cast<uint32_t *>(d_vals), d_idx);
+}
+
+int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int largest, int32_t *d_vals,
+                 int64_t *d_idx) {
+    if (!c || !d_keys || (!d_vals && !d_idx) || n < 1 || k < 1 || k > n) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    const u64 ntiles = ((u64)n + kth::TK_TILE - 1) / kth::TK_TILE;
+    const u64 nblk = (ntiles + kth::TK_TILES_PER_BLOCK - 1) / kth::TK_TILES_PER_BLOCK;
+    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2;
+    KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
+    // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
+    KTH_TRY(select_async(c, d_keys, n, largest ? n - k + 1 : k, nullptr, c->d_status));
+    const uint32_t *keys = reinterpret_cast<const uint32_t *>(d_keys);
+    const uint32_t flip = largest ? 0xFFFFFFFFu : 0u;
+    u64 *toff = c->topk, *bsum = toff + ntiles, *bbase = bsum + 2 * nblk, *meta = bbase + 2 * nblk;
+    uint32_t *tcnt = reinterpret_cast<uint32_t *>(meta + 2);
+    const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
+    const int waves = kth::TK_BLOCK / kth::WAVE;
+    const int g = (int)std::min<u64>((ntiles + waves - 1) / waves, (u64)c->num_cu * 32);
+    if (aligned)
+        kth::k_topk_count<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt);
+    else
+        kth::k_topk_count<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt);
+    kth::k_topk_reduce<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, bsum);
+    kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta);
+    kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
+    // write pass: one wave per 64 tiles
+    const int gw = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
+    if (aligned)
+        kth::k_topk_write<true><<<gw, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                    toff, bbase, meta, d_vals, d_idx);
+    else
+        kth::k_topk_write<false><<<gw, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                     toff, bbase, meta, d_vals, d_idx);
+    return launch_check();
 }
 
 int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, int64_t n_total, int dist, uint64_t seed,

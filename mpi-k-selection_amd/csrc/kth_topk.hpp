@@ -1,0 +1,261 @@
+// kth_topk.hpp -- top-k of one int32 array, gfx950.
+//
+// The k smallest (or largest) keys of n, with their int64 indices, written in
+// index order; of the keys equal to the k-th, the first ones by index.  The
+// reference has no top-k: its select block (kth-problem-seq.c:30-35) sorts and
+// reads one index, and sort(a)[:k] is the top-k it implies.  After the k-th
+// key v is known (select_async leaves it in d_status[0]), on 1024-key
+// "wave tiles" (one wavefront each, no barriers in the streaming kernels):
+//   k_topk_count   one streaming pass: per tile, #better-than-v | #equal << 16
+//   k_topk_reduce  per 4096 tiles: the block's two sums
+//   k_topk_scan    one workgroup: exclusive block bases, need = k - #better
+//   k_topk_down    per 4096 tiles: each tile's offsets inside its block
+//   k_topk_write   per tile that holds an output key: wave scan + scatter;
+//                  tiles without output never load their keys.
+// A kept key's slot is (#better before it) + min(#equal before it, need).
+#pragma once
+#include "kth_device.hpp"
+
+namespace kth {
+
+constexpr int TK_BLOCK = 256;
+constexpr int TK_TILE = 1024;                     // keys per wave tile
+constexpr int TK_KPL = TK_TILE / WAVE;            // 16 keys per lane
+constexpr int TK_SCAN_BLOCK = 1024;
+constexpr int TK_TILES_PER_BLOCK = TK_BLOCK * 16;  // reduce / down-sweep granularity (4096 tiles)
+// scratch (u64 words): tile counts (u32, ntiles), tile offsets (u64, ntiles),
+// block sums (2 per block), block bases (2 per block), meta [need, error]
+
+// order test against the k-th key: flip = 0 for smallest, ~0 for largest
+__device__ __forceinline__ bool tk_better(uint32_t u, uint32_t uv, uint32_t flip) { return (u ^ flip) < (uv ^ flip); }
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += dpp32<0x111, 0xF>(x);  // row_shr:1
+    x += dpp32<0x112, 0xF>(x);  // row_shr:2
+    x += dpp32<0x114, 0xF>(x);  // row_shr:4
+    x += dpp32<0x118, 0xF>(x);  // row_shr:8
+    x += dpp32<0x142, 0xA>(x);  // row_bcast:15
+    x += dpp32<0x143, 0xC>(x);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(x), WAVE - 1);
+}
+
+// Pass 1: tile t = keys [1024 t, 1024 t + 1024); tcnt[t] = #better | #equal << 16.
+// Lane l reads the 16-byte words l, l + 64, l + 128, l + 192 of its tile.
+template <bool ALIGNED>
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
+                                                         const int32_t *__restrict__ d_v, uint32_t flip,
+                                                         uint32_t *__restrict__ tcnt) {
+    const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
+    for (u64 t = (u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE; t < ntiles; t += nw) {
+        const u64 base = t * TK_TILE;
+        uint32_t c = 0;
+        auto one = [&](uint32_t x) {
+            const uint32_t u = key_of_i32(x);
+            c += tk_better(u, uv, flip) ? 1u : 0u;
+            c += u == uv ? 0x10000u : 0u;
+        };
+        if (ALIGNED && base + TK_TILE <= n) {
+            uint4 q[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q[r] = load_nt(reinterpret_cast<const uint4 *>(keys + base + r * 256 + lane * 4));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                one(q[r].x);
+                one(q[r].y);
+                one(q[r].z);
+                one(q[r].w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < TK_KPL; ++j) {
+                const u64 i = base + j * WAVE + lane;
+                if (i < n) one(keys[i]);
+            }
+        }
+        c = wave_sum32(c);
+        if (lane == 0) tcnt[t] = c;
+    }
+}
+
+// Pass 2: block b sums tiles [4096 b, 4096 b + 4096) -> bsum[2b] (better), bsum[2b+1] (equal).
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_reduce(const uint32_t *__restrict__ tcnt, u64 ntiles,
+                                                          u64 *__restrict__ bsum) {
+    const u64 t0 = (u64)blockIdx.x * TK_TILES_PER_BLOCK + threadIdx.x * 16;
+    u64 s = 0;
+    for (int j = 0; j < 16; ++j)
+        if (t0 + j < ntiles) {
+            const uint32_t c = tcnt[t0 + j];
+            s += (c & 0xFFFFu) | ((u64)(c >> 16) << 32);
+        }
+    __shared__ u64 wsum[TK_BLOCK / WAVE];
+    u64 tot;
+    block_exclusive_scan<TK_BLOCK>(s, wsum, &tot);  // per block < 2^32 keys: the halves cannot carry
+    if (threadIdx.x == 0) {
+        bsum[2 * blockIdx.x] = tot & 0xFFFFFFFFull;
+        bsum[2 * blockIdx.x + 1] = tot >> 32;
+    }
+}
+
+// Pass 3: one workgroup: bbase[2b], bbase[2b+1] = exclusive prefixes of the
+// better / equal block sums; meta[0] = need = k - #better; meta[1] = error
+// when the counts do not bracket k (cannot happen for a correct v).
+__global__ __launch_bounds__(TK_SCAN_BLOCK) void k_topk_scan(const u64 *__restrict__ cnt, int G, u64 k,
+                                                             u64 *__restrict__ base, u64 *__restrict__ meta) {
+    const int per = (G + TK_SCAN_BLOCK - 1) / TK_SCAN_BLOCK;
+    const int g0 = threadIdx.x * per;
+    u64 sb = 0, se = 0;
+    for (int j = 0; j < per; ++j)
+        if (g0 + j < G) {
+            sb += cnt[2 * (g0 + j)];
+            se += cnt[2 * (g0 + j) + 1];
+        }
+    __shared__ u64 wsum[TK_SCAN_BLOCK / WAVE];
+    u64 tb, te;
+    u64 pb = block_exclusive_scan<TK_SCAN_BLOCK>(sb, wsum, &tb);
+    u64 pe = block_exclusive_scan<TK_SCAN_BLOCK>(se, wsum, &te);
+    for (int j = 0; j < per; ++j)
+        if (g0 + j < G) {
+            base[2 * (g0 + j)] = pb;
+            base[2 * (g0 + j) + 1] = pe;
+            pb += cnt[2 * (g0 + j)];
+            pe += cnt[2 * (g0 + j) + 1];
+        }
+    if (threadIdx.x == 0) {
+        const bool ok = tb < k && k <= tb + te;
+        meta[0] = ok ? k - tb : 0;
+        meta[1] = ok ? 0 : 1;
+    }
+}
+
+// Pass 4: toff[t] = (#better | #equal << 32) in the tiles of t's block before t.
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restrict__ tcnt, u64 ntiles,
+                                                        u64 *__restrict__ toff) {
+    const u64 t0 = (u64)blockIdx.x * TK_TILES_PER_BLOCK + threadIdx.x * 16;
+    u64 v[16], s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t c = t0 + j < ntiles ? tcnt[t0 + j] : 0u;
+        v[j] = (c & 0xFFFFu) | ((u64)(c >> 16) << 32);
+        s += v[j];
+    }
+    __shared__ u64 wsum[TK_BLOCK / WAVE];
+    u64 p = block_exclusive_scan<TK_BLOCK>(s, wsum, nullptr);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (t0 + j < ntiles) {
+            toff[t0 + j] = p;
+            p += v[j];
+        }
+}
+
+// Pass 5: ordered compaction.  Each wave looks at 64 tiles at once (one per
+// lane) and visits only those holding output keys.  Lane l owns keys
+// [1024 t + 16 l, +16) of tile t, so a wave scan of the per-lane counts gives
+// every kept key its slot in the tile's output range, which is contiguous:
+// [bb + min(be, need), + #better + #kept ties).  The pairs are staged in the
+// wave's LDS and written out coalesced.
+template <bool ALIGNED>
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
+                                                         const int32_t *__restrict__ d_v, uint32_t flip,
+                                                         const uint32_t *__restrict__ tcnt,
+                                                         const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
+                                                         const u64 *__restrict__ meta, int32_t *__restrict__ vals,
+                                                         int64_t *__restrict__ idx) {
+    __shared__ uint32_t s_val[TK_BLOCK / WAVE][TK_TILE];
+    __shared__ uint16_t s_col[TK_BLOCK / WAVE][TK_TILE];
+    if (meta[1]) return;
+    const u64 need = meta[0];
+    const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
+    for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + w) * WAVE; tg < ntiles; tg += nw * WAVE) {
+        // lane l: tile tg + l's bases and whether it holds output keys
+        const u64 tl = tg + lane;
+        uint32_t c_l = 0;
+        u64 bb_l = 0, be_l = 0;
+        if (tl < ntiles) {
+            c_l = tcnt[tl];
+            const u64 off = toff[tl], blk = tl / TK_TILES_PER_BLOCK;
+            bb_l = bbase[2 * blk] + (off & 0xFFFFFFFFull);
+            be_l = bbase[2 * blk + 1] + (off >> 32);
+        }
+        const bool act = (c_l & 0xFFFFu) != 0 || ((c_l >> 16) != 0 && be_l < need);
+        u64 todo = __ballot(act);
+        while (todo) {
+            const int src = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const u64 t = tg + src;
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, src);
+            const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), src) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
+            const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
+            const u64 ce = c >> 16;
+            const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
+            const uint32_t total = (c & 0xFFFFu) + (uint32_t)take_e;  // this tile's output keys
+            const u64 start = bb + (be < need ? be : need);            // and where they go
+            const u64 i0 = t * TK_TILE + (u64)lane * TK_KPL;
+            uint32_t x[TK_KPL];
+            if (ALIGNED && t * TK_TILE + TK_TILE <= n) {
+#pragma unroll
+                for (int r = 0; r < TK_KPL / 4; ++r) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(keys + i0 + 4 * r);
+                    x[4 * r] = q.x;
+                    x[4 * r + 1] = q.y;
+                    x[4 * r + 2] = q.z;
+                    x[4 * r + 3] = q.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) x[j] = i0 + j < n ? keys[i0 + j] : 0u;
+            }
+            uint32_t mb = 0, me = 0;
+#pragma unroll
+            for (int j = 0; j < TK_KPL; ++j) {
+                const bool in = i0 + j < n;
+                const uint32_t u = key_of_i32(x[j]);
+                mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
+                me |= (uint32_t)(in && u == uv) << j;
+            }
+            const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
+            const uint32_t p = wave_incl_scan32(mine) - mine;
+            u64 b_before = bb + (p & 0xFFFFu);
+            u64 e_before = be + (p >> 16);
+            if (mb | me) {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) {
+                    u64 pos = ~0ull;
+                    if ((mb >> j) & 1) {
+                        pos = b_before + (e_before < need ? e_before : need);
+                        ++b_before;
+                    } else if ((me >> j) & 1) {
+                        if (e_before < need) pos = b_before + e_before;
+                        ++e_before;
+                    }
+                    if (pos != ~0ull) {
+                        const uint32_t r = (uint32_t)(pos - start);
+                        s_val[w][r] = x[j];
+                        s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
+                if (vals) vals[start + r] = (int32_t)s_val[w][r];
+                if (idx) idx[start + r] = (int64_t)(t * TK_TILE + s_col[w][r]);
+            }
+            __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
+        }
+    }
+}
+
+}  // namespace kth

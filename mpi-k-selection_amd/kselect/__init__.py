@@ -159,6 +159,14 @@ class Selector:
                  _ptr(d_vals) if d_vals is not None else None, _ptr(d_idx) if d_idx is not None else None),
               "kth_topk_rows")
 
+    def topk(self, d_keys, n, k, d_vals=None, d_idx=None, largest=False):
+        """The k smallest (largest=True: largest) int32 keys of n device keys and
+        their int64 indices, in index order, ties broken by index (kth_topk_i32;
+        asynchronous on the ctx stream)."""
+        check(LIB.kth_topk_i32(self._ctx, _ptr(d_keys), int(n), int(k), 1 if largest else 0,
+                               _ptr(d_vals) if d_vals is not None else None,
+                               _ptr(d_idx) if d_idx is not None else None), "kth_topk_i32")
+
     def fill(self, d_out, n, family=UNIFORM_FULL, seed=DEFAULT_SEED, param=0, offset=0, n_total=None):
         if isinstance(family, str):
             family = FAMILIES[family]

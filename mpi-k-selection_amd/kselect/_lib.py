@@ -92,6 +92,7 @@ PROTOS = {
                                          c_vp, c_vp]),
     "kth_topk_rows_f32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                                          c_vp, c_vp]),
+    "kth_topk_i32": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, c_vp, c_vp]),
     "kth_fill_synthetic": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                           ctypes.c_uint64, ctypes.c_int32]),
     "kth_dist_begin": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64]),

@@ -1,0 +1,109 @@
+"""GPU parity for the single-array top-k (kth_topk_i32).
+
+Contract (include/kth.h): the k smallest (largest) int32 keys with their int64
+indices, in index order; of the keys equal to the k-th, the first ones by
+index.  The reference implies this as sort(a)[:k] after its select block
+(kth-problem-seq.c:32-33); the restatement here is numpy's stable argsort
+(ties by index) re-sorted into index order.  Integer work: bit-exact.
+Large sizes are checked through size-independent properties (index order,
+vals == keys[idx], everything kept <= the k-th <= everything dropped, the tie
+quota taken first-by-index)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_idx(a, k, largest):
+    order = -a.astype(np.int64) if largest else a.astype(np.int64)
+    return np.sort(np.argsort(order, kind="stable")[:k])
+
+
+def _run(gpu, d, n, k, largest, with_vals=True, with_idx=True):
+    import torch
+    vals = torch.empty(k, dtype=torch.int32, device=d.device) if with_vals else None
+    idx = torch.empty(k, dtype=torch.int64, device=d.device) if with_idx else None
+    gpu.topk(d, n, k, vals, idx, largest=largest)
+    gpu.sync()
+    return vals, idx
+
+
+def _inputs(n, seed):
+    rng = np.random.default_rng(seed)
+    yield "uniform_full", rng.integers(-2 ** 31, 2 ** 31, size=n, dtype=np.int64).astype(np.int32)
+    yield "few_distinct", rng.integers(-3, 3, size=n).astype(np.int32)
+    yield "all_equal", np.full(n, 7, dtype=np.int32)
+    a = np.arange(n, dtype=np.int64)
+    yield "sorted_desc", (n - a).astype(np.int32)
+    b = rng.integers(-1000, 1000, size=n).astype(np.int32)
+    b[:: 3] = 2 ** 31 - 1
+    b[1:: 5] = -2 ** 31
+    yield "extremes", b
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 5000, 100003, (1 << 22) + 5])
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_vs_stable_sort(gpu, n, largest):
+    import torch
+    for fam, a in _inputs(n, n):
+        d = torch.from_numpy(a).cuda()
+        for k in sorted({k for k in (1, 2, 64, n // 2, n - 1, n) if 1 <= k <= n}):
+            vals, idx = _run(gpu, d, n, k, largest)
+            want = _ref_idx(a, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{fam} k={k}")
+            np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{fam} k={k}")
+
+
+def test_topk_unaligned_and_single_output(gpu):
+    import torch
+    n = 300001
+    rng = np.random.default_rng(3)
+    a = rng.integers(-50, 50, size=n + 3).astype(np.int32)
+    base = torch.from_numpy(a).cuda()
+    for off in (1, 2, 3):
+        d = base[off:off + n]
+        for largest in (False, True):
+            for k in (1, 777, n // 3):
+                want = _ref_idx(a[off:off + n], k, largest)
+                vals, _ = _run(gpu, d, n, k, largest, with_idx=False)
+                np.testing.assert_array_equal(vals.cpu().numpy(), a[off:off + n][want])
+                _, idx = _run(gpu, d, n, k, largest, with_vals=False)
+                np.testing.assert_array_equal(idx.cpu().numpy(), want)
+
+
+def test_topk_errors(gpu):
+    import kselect
+    import torch
+    d = torch.zeros(10, dtype=torch.int32, device="cuda")
+    out = torch.empty(10, dtype=torch.int32, device="cuda")
+    for n, k in ((10, 0), (10, 11), (0, 1)):
+        with pytest.raises(kselect.KthError):
+            gpu.topk(d, n, k, out, None)
+    with pytest.raises(kselect.KthError):
+        gpu.topk(d, 10, 1, None, None)
+
+
+@pytest.mark.parametrize("fam,k,largest", [("uniform_half", 64, False), ("uniform_full", 1 << 20, True),
+                                           ("few_distinct", (1 << 27) + 3, False), ("sorted_desc", 1000, True)])
+def test_topk_full_size_properties(gpu, fam, k, largest):
+    """2^28 keys (BASELINE-scale chunking, 1 GiB): properties that pin the exact top-k."""
+    import torch
+    n = 1 << 28
+    d = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu.fill(d, n, fam, param=7)
+    gpu.sync()
+    vals, idx = _run(gpu, d, n, k, largest)
+    idx_c = idx.cpu().numpy()
+    assert np.all(np.diff(idx_c) > 0) and idx_c[0] >= 0 and idx_c[-1] < n
+    assert torch.equal(vals, d[idx])
+    kth = gpu.select(d, n - k + 1 if largest else k)
+    sgn = -1 if largest else 1
+    dd = d.to(torch.int64) * sgn
+    v = kth * sgn
+    vv = vals.to(torch.int64) * sgn
+    assert int(vv.max()) == v  # the k-th is kept, nothing beyond it
+    n_better = int((dd < v).sum())
+    assert int((vv < v).sum()) == n_better  # every strictly better key is kept
+    # the ties kept are the first (k - n_better) ties by index
+    ties = torch.nonzero(dd == v).flatten()[: k - n_better].cpu().numpy()
+    np.testing.assert_array_equal(idx_c[(vv == v).cpu().numpy()], ties)
