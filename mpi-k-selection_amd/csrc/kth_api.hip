@@ -305,7 +305,8 @@ int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
 // The main pass + candidate levels + result, shared by the single-GPU window
 // path.  Expects the window state in st[0] and the last sample digit's
 // histogram in islot(0).
-int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status,
+               int tflag = 0, uint32_t *tflags = nullptr) {
     const int64_t s = sample_size(n);
     const u64 nchunks = ((u64)s + kth::SAMPLE_CHUNK - 1) / kth::SAMPLE_CHUNK;
     const u64 stride = (u64)n / nchunks;
@@ -338,7 +339,12 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.keys = keys;
     a.n_local = (u64)n;
     ev_main(c);
-    kth::k_main<<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand);
+    if (tflag == 1)
+        kth::k_main<1><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+    else if (tflag == 2)
+        kth::k_main<2><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+    else
+        kth::k_main<0><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
     ev_main(c);
     // decide + candidate (or fallback) levels.  The grids cover the fallback
     // (whole input); in the common case only the WGs the candidates need run.
@@ -360,7 +366,8 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     return launch_check();
 }
 
-int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status,
+                 int tflag = 0, uint32_t *tflags = nullptr) {
     if (!c || !d_keys || (!d_out && !d_status) || n < 1 || k < 1 || k > n) return KTH_EINVAL;
     KTH_TRY(set_device(c));
     if (c->dirty) {
@@ -374,7 +381,7 @@ int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_
     else if (n <= RADIX_MAX_N)
         rc = run_radix(c, d_keys, n, k, d_out, d_status);
     else
-        rc = run_window(c, d_keys, n, k, d_out, d_status);
+        rc = run_window(c, d_keys, n, k, d_out, d_status, tflag, tflags);
     ev_mark(c, c->ev_total, c->total_used);
     if (rc != KTH_OK) c->dirty = true;
     if (c->stamps) dump_stamps(c);
@@ -491,7 +498,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports here.
             int per = 4;
             hipFuncAttributes fa;
-            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kth::k_main)) == hipSuccess &&
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kth::k_main<0>)) == hipSuccess &&
                 fa.numRegs > 0) {
                 const int alloc = (fa.numRegs + 7) / 8 * 8;
                 const int by_vgpr = std::min(8, 512 / alloc);
@@ -738,31 +745,41 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     KTH_TRY(set_device(c));
     const u64 ntiles = ((u64)n + kth::TK_TILE - 1) / kth::TK_TILE;
     const u64 nblk = (ntiles + kth::TK_TILES_PER_BLOCK - 1) / kth::TK_TILES_PER_BLOCK;
-    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2;
+    // k_main's tile geometry (its flags cover the full tiles after the unaligned head)
+    u64 head = ((16u - (uint32_t)(reinterpret_cast<uintptr_t>(d_keys) & 15u)) & 15u) >> 2;
+    if (head > (u64)n) head = (u64)n;
+    const u64 nfull = (((u64)n - head) >> 2) / ((u64)kth::BLK * kth::MAIN_UNROLL);
+    const u64 fwords = 4 + nfull;
+    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2 + (fwords + 1) / 2;
     KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
+    uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + (words - (fwords + 1) / 2));
+    HIP_TRY(hipMemsetAsync(tflags, 0, 16, c->stream));  // window header: not valid until k_main<TF> runs
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
-    KTH_TRY(select_async(c, d_keys, n, largest ? n - k + 1 : k, nullptr, c->d_status));
+    // tile flags from the streaming pass pay off when few 1024-key tiles can hold output
+    const int tf = (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1) : 0;
+    KTH_TRY(select_async(c, d_keys, n, largest ? n - k + 1 : k, nullptr, c->d_status, tf, tflags));
     const uint32_t *keys = reinterpret_cast<const uint32_t *>(d_keys);
     const uint32_t flip = largest ? 0xFFFFFFFFu : 0u;
     u64 *toff = c->topk, *bsum = toff + ntiles, *bbase = bsum + 2 * nblk, *meta = bbase + 2 * nblk;
     uint32_t *tcnt = reinterpret_cast<uint32_t *>(meta + 2);
     const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
+    // count and write passes: one wave per 64 tiles
     const int waves = kth::TK_BLOCK / kth::WAVE;
-    const int g = (int)std::min<u64>((ntiles + waves - 1) / waves, (u64)c->num_cu * 32);
+    const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
     if (aligned)
-        kth::k_topk_count<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt);
+        kth::k_topk_count<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                     tflags, head, nfull);
     else
-        kth::k_topk_count<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt);
+        kth::k_topk_count<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                     tflags, head, nfull);
     kth::k_topk_reduce<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, bsum);
     kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta);
     kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
-    // write pass: one wave per 64 tiles
-    const int gw = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
     if (aligned)
-        kth::k_topk_write<true><<<gw, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+        kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                     toff, bbase, meta, d_vals, d_idx);
     else
-        kth::k_topk_write<false><<<gw, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+        kth::k_topk_write<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                      toff, bbase, meta, d_vals, d_idx);
     return launch_check();
 }
@@ -859,7 +876,7 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
-    kth::k_main<<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand);
+    kth::k_main<0><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
     ev_main(c);
     c->dist_level_next = 0;
     KTH_TRY(launch_check());

@@ -564,7 +564,14 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
     }
 }
 
-__global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out) {
+// TF (top-k variant, kth_topk.hpp): 0 = plain select; 1 / 2 = also record, per
+// full tile and wave, one byte "some key <= hi" (1, k smallest) or "some key
+// >= lo" (2, k largest) at ((uint8_t *)(tflags + 4))[4 * tile + wave], and the
+// window as tflags[0..2] = {lo, hi, 1} (signed).  A tile whose word is zero
+// holds no output key of the top-k when its k-th lies inside the window.
+template <int TF>
+__global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out,
+                                              uint32_t *__restrict__ tflags) {
     constexpr int U = MAIN_UNROLL, S = MAIN_SUB, K = 4 * S;
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
@@ -578,6 +585,13 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     if (ss.mode != MODE_MAIN) return;  // block-uniform (error or resolved)
     const int32_t slo = i32_of_key(ss.lo), shi = i32_of_key(ss.hi);
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    if constexpr (TF != 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            tflags[0] = (uint32_t)slo;
+            tflags[1] = (uint32_t)shi;
+            tflags[2] = 1u;
+        }
+    }
     Stager st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
 
@@ -613,6 +627,17 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         uint4 x[U];
         load_tile(x, t);
         scan_tile(x);
+        if constexpr (TF != 0) {
+            bool nr = false;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t q[4] = {(int32_t)x[u].x, (int32_t)x[u].y, (int32_t)x[u].z, (int32_t)x[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) nr |= TF == 1 ? q[j] <= shi : q[j] >= slo;
+            }
+            const unsigned long long B = __builtin_amdgcn_ballot_w64(nr);
+            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = B ? 1u : 0u;
+        }
     }
     // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;

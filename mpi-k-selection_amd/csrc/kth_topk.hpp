@@ -6,7 +6,9 @@
 // reads one index, and sort(a)[:k] is the top-k it implies.  After the k-th
 // key v is known (select_async leaves it in d_status[0]), on 1024-key
 // "wave tiles" (one wavefront each, no barriers in the streaming kernels):
-//   k_topk_count   one streaming pass: per tile, #better-than-v | #equal << 16
+//   k_topk_count   per tile, #better-than-v | #equal << 16; reads only the
+//                  tiles the select's own streaming pass flagged as possibly
+//                  holding output (k_main<TF>), all tiles otherwise
 //   k_topk_reduce  per 4096 tiles: the block's two sums
 //   k_topk_scan    one workgroup: exclusive block bases, need = k - #better
 //   k_topk_down    per 4096 tiles: each tile's offsets inside its block
@@ -48,41 +50,83 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
 
 // Pass 1: tile t = keys [1024 t, 1024 t + 1024); tcnt[t] = #better | #equal << 16.
 // Lane l reads the 16-byte words l, l + 64, l + 128, l + 192 of its tile.
+// Tiles the select's streaming pass proved empty of output are skipped: when
+// k_main<TF> ran (tflags[2] == 1) and v lies on the window's near side of its
+// far edge, a tile inside k_main's full tiles (MT keys each, after `head`
+// unaligned keys; nfull of them) whose flag words are zero has no key <= v
+// (>= v for largest): count 0, no loads.
+constexpr u64 TK_MAIN_TILE = (u64)BLK * MAIN_UNROLL * 4;  // keys per k_main tile
+
 template <bool ALIGNED>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
-                                                         uint32_t *__restrict__ tcnt) {
+                                                         uint32_t *__restrict__ tcnt,
+                                                         const uint32_t *__restrict__ tflags, u64 head, u64 nfull) {
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
-    for (u64 t = (u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE; t < ntiles; t += nw) {
-        const u64 base = t * TK_TILE;
-        uint32_t c = 0;
-        auto one = [&](uint32_t x) {
-            const uint32_t u = key_of_i32(x);
-            c += tk_better(u, uv, flip) ? 1u : 0u;
-            c += u == uv ? 0x10000u : 0u;
-        };
-        if (ALIGNED && base + TK_TILE <= n) {
-            uint4 q[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) q[r] = load_nt(reinterpret_cast<const uint4 *>(keys + base + r * 256 + lane * 4));
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                one(q[r].x);
-                one(q[r].y);
-                one(q[r].z);
-                one(q[r].w);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < TK_KPL; ++j) {
-                const u64 i = base + j * WAVE + lane;
-                if (i < n) one(keys[i]);
+    const bool skip_ok = tflags[2] == 1u && (flip == 0u ? d_v[0] <= (int32_t)tflags[1] : d_v[0] >= (int32_t)tflags[0]);
+    const uint32_t *fw = tflags + 4;
+    // each wave takes 64 tiles at a time: lane l tests tile tg + l's flags, the
+    // wave then streams only the tiles that may hold output
+    for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE) * WAVE; tg < ntiles; tg += nw * WAVE) {
+        const u64 tl = tg + lane;
+        bool act = tl < ntiles;
+        if (act && skip_ok && tl * TK_TILE >= head) {
+            const u64 b0 = tl * TK_TILE, last = (b0 + TK_TILE < n ? b0 + TK_TILE : n) - 1;
+            const u64 ta = (b0 - head) / TK_MAIN_TILE, tb = (last - head) / TK_MAIN_TILE;
+            if (tb < nfull && (fw[ta] | fw[tb]) == 0u) {
+                act = false;
+                tcnt[tl] = 0u;
             }
         }
-        c = wave_sum32(c);
-        if (lane == 0) tcnt[t] = c;
+        u64 todo = __ballot(act);
+        while (todo) {  // two tiles per round: 8 loads in flight per lane
+            const u64 t1 = tg + __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const bool two = todo != 0;
+            const u64 t2 = two ? tg + __builtin_ctzll(todo) : t1;
+            if (two) todo &= todo - 1;
+            uint32_t c1 = 0, c2 = 0;
+            auto one = [&](uint32_t &c, uint32_t x) {
+                const uint32_t u = key_of_i32(x);
+                c += tk_better(u, uv, flip) ? 1u : 0u;
+                c += u == uv ? 0x10000u : 0u;
+            };
+            const u64 b1 = t1 * TK_TILE, b2 = t2 * TK_TILE;
+            if (ALIGNED && b1 + TK_TILE <= n && b2 + TK_TILE <= n) {
+                uint4 q[8];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    q[r] = load_nt(reinterpret_cast<const uint4 *>(keys + b1 + r * 256 + lane * 4));
+                    q[4 + r] = load_nt(reinterpret_cast<const uint4 *>(keys + b2 + r * 256 + lane * 4));
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    one(c1, q[r].x);
+                    one(c1, q[r].y);
+                    one(c1, q[r].z);
+                    one(c1, q[r].w);
+                    one(c2, q[4 + r].x);
+                    one(c2, q[4 + r].y);
+                    one(c2, q[4 + r].z);
+                    one(c2, q[4 + r].w);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) {
+                    const u64 i1 = b1 + j * WAVE + lane, i2 = b2 + j * WAVE + lane;
+                    if (i1 < n) one(c1, keys[i1]);
+                    if (i2 < n) one(c2, keys[i2]);
+                }
+            }
+            c1 = wave_sum32(c1);
+            c2 = wave_sum32(c2);
+            if (lane == 0) {
+                tcnt[t1] = c1;
+                if (two) tcnt[t2] = c2;
+            }
+        }
     }
 }
 

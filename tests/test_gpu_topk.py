@@ -107,3 +107,24 @@ def test_topk_full_size_properties(gpu, fam, k, largest):
     # the ties kept are the first (k - n_better) ties by index
     ties = torch.nonzero(dd == v).flatten()[: k - n_better].cpu().numpy()
     np.testing.assert_array_equal(idx_c[(vv == v).cpu().numpy()], ties)
+
+
+def test_topk_window_path_unaligned_small_k(gpu):
+    """n > 4 Mi takes the window path, whose streaming pass flags the tiles that
+    can hold output (k * 1024 <= n): unaligned heads, a ragged tail, clustered keys."""
+    import torch
+    n = (1 << 23) + 3
+    rng = np.random.default_rng(11)
+    a = rng.integers(-2 ** 31, 2 ** 31, size=n + 3, dtype=np.int64).astype(np.int32)
+    a[5_000_000:5_000_100] = -2 ** 31  # a cluster of minima inside one tile
+    a[-40:] = 2 ** 31 - 1              # maxima in the ragged tail
+    base = torch.from_numpy(a).cuda()
+    for off in (0, 1, 3):
+        d = base[off:off + n]
+        h = a[off:off + n]
+        for largest in (False, True):
+            for k in (1, 37, 100, 4096, 8191):
+                vals, idx = _run(gpu, d, n, k, largest)
+                want = _ref_idx(h, k, largest)
+                np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"off={off} k={k} {largest}")
+                np.testing.assert_array_equal(vals.cpu().numpy(), h[want])
