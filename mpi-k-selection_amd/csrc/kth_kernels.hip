@@ -626,17 +626,17 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         load_tile(x, t);
+        // the flag falls out of the counters: "some key <= hi" = some key counted
+        // below / at lo, at hi, or staged inside; "some key >= lo" = not all
+        // 4 * U of the lane's keys counted below lo
+        const uint32_t c0 = TF == 1 ? clt + ceqlo + ceqhi : clt;
+        const u64 w0 = st.winside;
         scan_tile(x);
         if constexpr (TF != 0) {
-            bool nr = false;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t q[4] = {(int32_t)x[u].x, (int32_t)x[u].y, (int32_t)x[u].z, (int32_t)x[u].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) nr |= TF == 1 ? q[j] <= shi : q[j] >= slo;
-            }
+            const bool nr = TF == 1 ? (clt + ceqlo + ceqhi != c0) : (clt - c0 != 4u * U);
             const unsigned long long B = __builtin_amdgcn_ballot_w64(nr);
-            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = B ? 1u : 0u;
+            const bool any = B != 0 || (TF == 1 && st.winside != w0);
+            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = any ? 1u : 0u;
         }
     }
     // ragged end: the last partial tile, as masked groups of one workgroup
