@@ -565,10 +565,12 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 }
 
 // TF (top-k variant, kth_topk.hpp): 0 = plain select; 1 / 2 = also record, per
-// full tile and wave, one byte "some key <= hi" (1, k smallest) or "some key
-// >= lo" (2, k largest) at ((uint8_t *)(tflags + 4))[4 * tile + wave], and the
-// window as tflags[0..2] = {lo, hi, 1} (signed).  A tile whose word is zero
-// holds no output key of the top-k when its k-th lies inside the window.
+// full tile, wave and row (the tile's u-th run of 4 * BLK keys), one bit "some
+// key <= hi" (1, k smallest) or "some key >= lo" (2, k largest): bit u of
+// ((uint8_t *)(tflags + 4))[4 * tile + wave]; and the window as tflags[0..2] =
+// {lo, hi, 1} (signed).  A row with no bit set in any wave holds no output key
+// of the top-k when its k-th lies inside the window.
+static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot in a byte");
 template <int TF>
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out,
                                               uint32_t *__restrict__ tflags) {
@@ -626,17 +628,18 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         load_tile(x, t);
-        // the flag falls out of the counters: "some key <= hi" = some key counted
-        // below / at lo, at hi, or staged inside; "some key >= lo" = not all
-        // 4 * U of the lane's keys counted below lo
-        const uint32_t c0 = TF == 1 ? clt + ceqlo + ceqhi : clt;
-        const u64 w0 = st.winside;
         scan_tile(x);
         if constexpr (TF != 0) {
-            const bool nr = TF == 1 ? (clt + ceqlo + ceqhi != c0) : (clt - c0 != 4u * U);
-            const unsigned long long B = __builtin_amdgcn_ballot_w64(nr);
-            const bool any = B != 0 || (TF == 1 && st.winside != w0);
-            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = any ? 1u : 0u;
+            // bit u of the wave's byte: some key of row u (the tile's u-th run of
+            // 4 * BLK keys) in this wave's part is <= hi (TF 1) / >= lo (TF 2)
+            uint32_t rows = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t a0 = (int32_t)x[u].x, a1 = (int32_t)x[u].y, a2 = (int32_t)x[u].z, a3 = (int32_t)x[u].w;
+                const bool nr = TF == 1 ? min(min(a0, a1), min(a2, a3)) <= shi : max(max(a0, a1), max(a2, a3)) >= slo;
+                rows |= (__builtin_amdgcn_ballot_w64(nr) != 0 ? 1u : 0u) << u;
+            }
+            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = (uint8_t)rows;
         }
     }
     // ragged end: the last partial tile, as masked groups of one workgroup

@@ -52,10 +52,13 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
 // Lane l reads the 16-byte words l, l + 64, l + 128, l + 192 of its tile.
 // Tiles the select's streaming pass proved empty of output are skipped: when
 // k_main<TF> ran (tflags[2] == 1) and v lies on the window's near side of its
-// far edge, a tile inside k_main's full tiles (MT keys each, after `head`
-// unaligned keys; nfull of them) whose flag words are zero has no key <= v
-// (>= v for largest): count 0, no loads.
-constexpr u64 TK_MAIN_TILE = (u64)BLK * MAIN_UNROLL * 4;  // keys per k_main tile
+// far edge, a tile inside k_main's full tiles (rows of TK_MAIN_ROW keys after
+// `head` unaligned keys; MAIN_UNROLL rows per tile, nfull tiles) whose rows
+// carry no flag bit has no key <= v (>= v for largest): count 0, no loads.
+constexpr u64 TK_MAIN_ROW = (u64)BLK * 4;  // keys per k_main row (one 16-B load per thread)
+__device__ __forceinline__ bool tk_row_flagged(const uint32_t *fw, u64 r) {
+    return (fw[r / MAIN_UNROLL] & (0x01010101u << (r % MAIN_UNROLL))) != 0u;
+}
 
 template <bool ALIGNED>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
@@ -74,8 +77,8 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
         bool act = tl < ntiles;
         if (act && skip_ok && tl * TK_TILE >= head) {
             const u64 b0 = tl * TK_TILE, last = (b0 + TK_TILE < n ? b0 + TK_TILE : n) - 1;
-            const u64 ta = (b0 - head) / TK_MAIN_TILE, tb = (last - head) / TK_MAIN_TILE;
-            if (tb < nfull && (fw[ta] | fw[tb]) == 0u) {
+            const u64 ra = (b0 - head) / TK_MAIN_ROW, rb = (last - head) / TK_MAIN_ROW;
+            if (rb / MAIN_UNROLL < nfull && !tk_row_flagged(fw, ra) && !tk_row_flagged(fw, rb)) {
                 act = false;
                 tcnt[tl] = 0u;
             }
