@@ -82,6 +82,16 @@ def test_no_cpu_fallback(lib):
     assert v.kth_select(5) == -3  # VecKthSelect's device-error sentinel
 
 
+def test_topk_argument_checks(lib):
+    """kth_topk_i32 validates before touching a device (include/kth.h contract)."""
+    import kselect
+    a = np.arange(16, dtype=np.int32)
+    out = np.zeros(16, dtype=np.int32)
+    for n, k in ((16, 0), (16, 17), (0, 1)):
+        assert lib.kth_topk_i32(None, a.ctypes.data, n, k, 0, out.ctypes.data, None) == kselect.KTH_EINVAL
+    assert lib.kth_topk_i32(None, a.ctypes.data, 16, 1, 0, None, None) == kselect.KTH_EINVAL
+
+
 def test_missing_library_is_loud():
     code = ("import sys; sys.path.insert(0, %r); import kselect" % PKG)
     p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, KTH_LIB="/nonexistent/libkth.so"),
