@@ -52,78 +52,195 @@ def cpu_model():
     return platform.processor()
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, one
+    GPU each), replacing the reference's `mpirun -n P` launch
+    (TODO-kth-problem-cgm.c:53-61).  This parent never imports torch or touches a
+    GPU; it forwards the ranks' output, stops every rank when one fails, and
+    exits with the first failing rank's code."""
+    port = _free_port()
+    log(f"bench: launching {n} ranks (one per GPU), rendezvous 127.0.0.1:{port}")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(enumerate(procs))
+    while live:
+        time.sleep(0.2)
+        for item in list(live):
+            r, p = item
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(item)
+            if code != 0:
+                log(f"bench: rank {r} exited with code {code}; stopping the other ranks")
+                rc = rc or code
+                for _, q in live:
+                    q.terminate()
+    return rc
+
+
+def need_gpu(local_rank):
+    """Fail loudly (there is no CPU fallback) unless GPU `local_rank` is visible."""
+    import torch
+
+    ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if local_rank >= ndev:
+        raise SystemExit(f"bench: rank needs GPU {local_rank} but {ndev} GPU(s) are visible (no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    return torch.device("cuda", local_rank)
+
+
 class _IntVector(ctypes.Structure):  # reference vector.h:7-11
     _fields_ = [("size", ctypes.c_int), ("capacity", ctypes.c_int), ("data", ctypes.POINTER(ctypes.c_int))]
 
 
-def cpu_baseline(keys_np, family):
-    """The reference's seq select block (kth-problem-seq.c:30-35: VecQuickSort + VecGet
-    on one core) timed on this host on a bounded sample of the workload."""
+def cpu_host():
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count()
+    return {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+def cpu_baseline(keys_np, family, min_seconds=5.0, max_reps=50):
+    """The reference's seq select block (kth-problem-seq.c:30-35: VecQuickSort +
+    VecGet(k-1) on one core), timed on this host.  BASELINE config 1: 2^20 keys,
+    k = n/2.  Each repetition sorts a fresh copy; reported: median over the
+    repetitions of the monotonic time and of the CPU time (clock(), what the
+    reference prints, kth-problem-seq.c:30,35)."""
     import numpy as np
 
     n = keys_np.size
     k = n // 2
     ref = os.path.join(REPO, "oracle", "_ref", "libvector_ref.so")
-    buf = np.array(keys_np, dtype=np.int32, copy=True)
     if os.path.exists(ref):
         lib = ctypes.CDLL(ref)
         lib.VecGet.restype = ctypes.c_int
-        v = _IntVector(n, n, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
-        t0 = time.perf_counter()
-        lib.VecQuickSort(ctypes.byref(v))
-        ans = lib.VecGet(ctypes.byref(v), ctypes.c_int(k - 1))
-        dt = time.perf_counter() - t0
         kind = "reference"
-        what = "reference vector.c (oracle/_ref/libvector_ref.so): VecQuickSort + VecGet(k-1)"
+        what = "reference vector.c compiled from its own source (oracle/_ref/libvector_ref.so): VecQuickSort + VecGet(k-1)"
+
+        def run(buf):
+            v = _IntVector(n, n, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            lib.VecQuickSort(ctypes.byref(v))
+            return lib.VecGet(ctypes.byref(v), ctypes.c_int(k - 1))
     else:
         lib = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
         lib.ko_seq_ref_inplace.restype = ctypes.c_int32
         lib.ko_seq_ref_inplace.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]
-        t0 = time.perf_counter()
-        ans = lib.ko_seq_ref_inplace(buf.ctypes.data, n, k)
-        dt = time.perf_counter() - t0
         kind = "port"
-        what = "oracle restatement ko_seq_ref_inplace (qsort + VecGet)"
+        what = "oracle restatement ko_seq_ref_inplace (qsort with the reference comparator + VecGet)"
+
+        def run(buf):
+            return lib.ko_seq_ref_inplace(buf.ctypes.data, n, k)
+    mono, cpu, answers = [], [], set()
+    while len(mono) < 3 or (sum(mono) < min_seconds and len(mono) < max_reps):
+        buf = np.array(keys_np, dtype=np.int32, copy=True)
+        c0, t0 = time.thread_time(), time.monotonic()
+        answers.add(int(run(buf)))
+        t1, c1 = time.monotonic(), time.thread_time()
+        mono.append(t1 - t0)
+        cpu.append(c1 - c0)
+    dt, dc = float(np.median(mono)), float(np.median(cpu))
+    want = int(np.partition(keys_np, k - 1)[k - 1])
     return {
         "value": n / dt / 1e9,
         "unit": "Gkeys/s",
         "cores": 1,
         "kind": kind,
-        "sample": f"seq select block, {what}, on 2^{n.bit_length() - 1} keys of {family}, k=n/2, "
-                  f"{dt:.2f} s; host {cpu_model()} ({os.cpu_count()} cpus visible)",
-        "seconds": dt,
-        "answer": int(ans),
+        "sample": f"BASELINE config 1: seq select block, {what}, 2^{n.bit_length() - 1} keys of {family}, k=n/2; "
+                  f"median of {len(mono)} runs: {dt * 1e3:.1f} ms monotonic, {dc * 1e3:.1f} ms clock()",
+        "n": n,
+        "reps": len(mono),
+        "seconds_monotonic": dt,
+        "seconds_clock": dc,
+        "answer": answers.pop() if len(answers) == 1 else sorted(answers),
+        "want": want,
     }
 
 
-def cpu_baseline_cgm(keys_np, procs, timeout=120):
-    """The reference CGM program (TODO-kth-problem-cgm.c, n/k parameterised) under mpirun."""
+def cpu_baseline_cgm(keys_np, procs, reps=3, timeout=120):
+    """The reference CGM program (TODO-kth-problem-cgm.c compiled from its own
+    source, n/k read from the environment: oracle/_ref/cgm_param) under
+    `mpirun -n procs`; its own MPI_Wtime from before the Scatterv to the answer
+    (:76, :279).  Median of `reps` runs.  Raises on any failure."""
+    import re
+
+    import numpy as np
+
     binary = os.path.join(REPO, "oracle", "_ref", "cgm_param")
     mpirun = "/opt/conda/bin/mpirun"
-    if not (os.path.exists(binary) and os.path.exists(mpirun)):
-        return None
+    for f in (binary, mpirun):
+        if not os.path.exists(f):
+            raise RuntimeError(f"CGM baseline: {f} missing")
     n = keys_np.size
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         keys_np.astype("<i4").tofile(f)
         path = f.name
+    times, answers = [], set()
     try:
         env = dict(os.environ, KO_N=str(n), KO_K=str(n // 2), KO_TIME="1", KO_INPUT=path)
-        p = subprocess.run([mpirun, "-n", str(procs), binary], env=env, capture_output=True, text=True,
-                           timeout=timeout)
-        import re
-
-        m = re.search(r"kth element[= ]\s*(-?\d+)\s*\n\s*time:\s*([0-9.]+)", p.stdout)
-        if not m:
-            return {"error": (p.stdout + p.stderr)[-300:]}
-        t = float(m.group(2))
-        return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": procs, "kind": "reference",
-                "sample": f"mpirun -n {procs} CGM (oracle/_ref/cgm_param) on 2^{n.bit_length() - 1} keys, k=n/2, "
-                          f"MPI_Wtime {t:.3f} s (TODO-kth-problem-cgm.c:76,279)",
-                "answer": int(m.group(1))}
-    except subprocess.TimeoutExpired:
-        return {"error": f"timeout {timeout}s"}
+        for _ in range(reps):
+            p = subprocess.run([mpirun, "-n", str(procs), binary], env=env, capture_output=True, text=True,
+                               timeout=timeout, stdin=subprocess.DEVNULL)
+            m = re.search(r"kth element[= ]\s*(-?\d+)\s*\n\s*time:\s*([0-9.]+)", p.stdout)
+            if not m:
+                raise RuntimeError(f"CGM baseline P={procs}: no answer line (rc {p.returncode}): "
+                                   f"{(p.stdout + p.stderr)[-300:]!r}")
+            answers.add(int(m.group(1)))
+            times.append(float(m.group(2)))
     finally:
         os.unlink(path)
+    t = float(np.median(times))
+    return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": procs, "procs": procs, "kind": "reference",
+            "sample": f"mpirun -n {procs} reference CGM (oracle/_ref/cgm_param) on 2^{n.bit_length() - 1} keys, "
+                      f"k=n/2, median MPI_Wtime of {reps} runs {t * 1e3:.1f} ms (TODO-kth-problem-cgm.c:76,279)",
+            "seconds": t, "reps": reps, "answer": answers.pop() if len(answers) == 1 else sorted(answers)}
+
+
+def cpu_baselines(keys_np, family):
+    """Every CPU baseline of BASELINE.md on this host, errors collected rather
+    than swallowed: (cpu_baseline, cpu_baseline_cgm list, errors)."""
+    import numpy as np
+
+    want = int(np.partition(keys_np, keys_np.size // 2 - 1)[keys_np.size // 2 - 1])
+    errors, seq, cgm = [], None, []
+    try:
+        seq = cpu_baseline(keys_np, family)
+        seq["answer_ok"] = seq["answer"] == want
+        if not seq["answer_ok"]:
+            errors.append(f"seq baseline answered {seq['answer']}, true k-th is {want}")
+    except Exception as e:  # noqa: BLE001 -- reported at the top level of the line
+        errors.append(f"seq baseline: {e!r}")
+    host = cpu_host()
+    share = min(16, host["affinity_cpus"] or 1)  # the GPU box's CPU share is 16 per GPU
+    for P in sorted({2, 4, 8, share}):
+        try:
+            r = cpu_baseline_cgm(keys_np, P)
+            r["answer_ok"] = r["answer"] == want
+            if not r["answer_ok"]:
+                errors.append(f"CGM baseline P={P} answered {r['answer']}, true k-th is {want}")
+            cgm.append(r)
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"CGM baseline P={P}: {e!r}")
+    if seq is not None:
+        seq.pop("want", None)
+        seq["sample"] += f"; host {host['cpu_model']}, nproc {host['nproc']}, affinity {host['affinity_cpus']} cpus"
+    return seq, cgm, errors, host
 
 
 def rows_main(args):
@@ -138,8 +255,7 @@ def rows_main(args):
 
     import kselect
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = need_gpu(local_rank)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     if world > 1:
@@ -239,8 +355,7 @@ def topk_main(args):
 
     import kselect
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = need_gpu(local_rank)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     if world > 1:
@@ -306,7 +421,7 @@ def main():
     ap.add_argument("--family", default="uniform_half")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
     ap.add_argument("--k", type=int, default=0, help="global 1-based rank (default n_total/2)")
-    ap.add_argument("--cpu-log2n", type=int, default=25)
+    ap.add_argument("--cpu-log2n", type=int, default=20, help="CPU baseline size (BASELINE config 1: 2^20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="run the sharded (kth_dist_* + RCCL) protocol even on one GPU")
@@ -317,14 +432,28 @@ def main():
     ap.add_argument("--cols", type=int, default=4096)
     ap.add_argument("--rows-dtype", choices=["i32", "f32"], default="i32")
     ap.add_argument("--topk", action="store_true", help="rows workload: top-k (largest) values + columns per row")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help="(tests) each rank prints its launch environment as JSON and exits before touching a GPU")
     args = ap.parse_args()
+    if args.gpus < 1:
+        log(f"bench: --gpus {args.gpus} must be >= 1")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run as {args.gpus}")
+        return 2
+    if args.probe_launch:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                          "MASTER_PORT")}), flush=True)
+        return 0
     if args.workload == "rows":
         return rows_main(args)
     if args.workload == "topk":
         return topk_main(args)
 
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
 
     import torch
@@ -333,8 +462,7 @@ def main():
     import kselect
     from kselect.dist import DistSelector, HipBackend
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = need_gpu(local_rank)
     # one explicit stream for everything (torch ops, the selector, RCCL): the
     # legacy null stream would add implicit synchronisation to every launch
     torch.cuda.set_stream(torch.cuda.Stream(dev))
@@ -357,6 +485,7 @@ def main():
     keys = torch.empty(n_local, dtype=torch.int32, device=dev)
     sel.fill(keys, n_local, family, args.seed, offset=rank * n_local, n_total=n_total)
     out = torch.zeros(args.warmup + args.steps, dtype=torch.int32, device=dev)
+    comm_world = None
 
     if not sharded:
         sel.reserve(n_local)
@@ -365,6 +494,9 @@ def main():
             sel.select_async(keys, n_local, k, out[i:i + 1])
     else:
         ds = DistSelector(HipBackend(local_rank, sel))
+        comm_world = getattr(ds.comm, "world", None)
+        if comm_world != world:
+            raise SystemExit(f"bench: RCCL communicator spans {comm_world} ranks, WORLD_SIZE is {world}")
 
         def step(i):
             ds.select(keys, n_local, n_total, k, out=out[i:i + 1])
@@ -433,6 +565,7 @@ def main():
             "keys_per_gpu": n_local,
             "family": args.family,
             "parallelism": f"shards{world}" if sharded else "single",
+            "rccl_world": comm_world if sharded else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -459,13 +592,11 @@ def main():
         sel.fill(tmp, nc, family, args.seed, offset=0, n_total=nc)
         keys_np = tmp.cpu().numpy()
         del tmp
-        try:
-            res["cpu_baseline"] = cpu_baseline(keys_np, args.family)
-            cg = cpu_baseline_cgm(keys_np, min(8, os.cpu_count() or 1))
-            if cg:
-                res["cpu_baseline_cgm"] = cg
-        except Exception as e:  # noqa: BLE001 -- baseline is informational
-            res["cpu_baseline"] = {"error": repr(e)}
+        seq, cgm, errors, host = cpu_baselines(keys_np, args.family)
+        res["cpu_baseline"] = seq
+        res["cpu_baseline_cgm"] = cgm
+        res["cpu_baseline_errors"] = errors
+        res["cpu_host"] = host
 
     if rank == 0:
         print(json.dumps(res), flush=True)

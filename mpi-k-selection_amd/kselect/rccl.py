@@ -117,6 +117,7 @@ class TorchComm:
 
     def __init__(self, group=None):
         self.group = group
+        self.world = dist.get_world_size(group)
 
     def all_reduce_sum_(self, t):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
