@@ -41,6 +41,7 @@ extern "C" {
 #define KTH_EHIP (-3)     /* HIP runtime or kernel launch error         */
 #define KTH_ENODEV (-4)   /* no HIP device                              */
 #define KTH_EINTERNAL (-5) /* device-side consistency check failed      */
+#define KTH_ECOMM (-6)    /* RCCL missing or a collective failed        */
 
 #define KTH_VERSION 1
 
@@ -191,6 +192,42 @@ int64_t kth_dist_sample_size(int64_t n);
  * ceil(s / C) chunks of C = kth_sample_chunk() consecutive keys, chunk c at
  * key c * (n / ceil(s / C)); the last chunk holds the remaining s mod C keys. */
 int kth_sample_chunk(void);
+/* Window half-width in sample standard deviations: the window ranks in a
+ * sample of s keys for rank k of n are p*s -+ (z*sqrt(s*p*(1-p)) + 2), p = k/n
+ * (KTH_WINDOW_Z overrides the built-in 5.0). */
+double kth_window_z(void);
+/* Candidate-buffer capacity (keys) of a streaming pass over n_local keys:
+ * max(2^20, n_local / 32); more candidates than this on a rank set its
+ * overflow count and the selection takes the exact fallback levels. */
+int64_t kth_dist_cand_capacity(int64_t n_local);
+
+/* --- sharded selection, one process driving several GPUs ---------------------
+ * Replaces TODO-kth-problem-cgm.c:81-278 (block partition + Scatterv, the
+ * weighted-median rounds, final Gatherv + rank-0 sort) for a caller holding one
+ * shard per GPU in a single process: the kth_dist_* steps for every device,
+ * with the collectives as grouped RCCL calls over communicators from
+ * ncclCommInitAll (RCCL is dlopen'ed at first use: the librccl.so.1 already in
+ * the process, else the system one; KTH_ECOMM if neither loads).
+ *   kth_sharded_create      devices[0..ngpu) distinct; one ctx, stream and
+ *                           communicator per device
+ *   kth_sharded_select_i32  shard i = shards[i][0..shard_n[i]) in device
+ *                           devices[i]'s memory; k-th smallest (1-based) of the
+ *                           union -> *out (host).  Synchronous; the shards must
+ *                           be complete when it is called (it does not order
+ *                           against the caller's streams).  Shards of fewer
+ *                           than 64 keys: the union is copied to device 0 and
+ *                           selected there.  Any shard sizes are exact;
+ *                           balanced shards (n/P + (i < n%P)) are the fast case.
+ *   kth_select_i32_sharded  one-shot form; each shard's device is taken from
+ *                           its pointer (device memory only), the handle is
+ *                           cached per host thread for the same device list. */
+typedef struct kth_sharded kth_sharded;
+int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out);
+int kth_sharded_destroy(kth_sharded *h);
+int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const int64_t *shard_n, int64_t k,
+                           int32_t *out);
+int kth_select_i32_sharded(const int32_t *const *dev_shards, const int64_t *shard_n, int ngpu, int64_t k,
+                           int32_t *out);
 
 #ifdef __cplusplus
 }

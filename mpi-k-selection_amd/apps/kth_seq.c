@@ -7,7 +7,8 @@
  * reference build), same IntVector container, same output format
  * ("Solution found solution=%d \ntime: %f\n", :37) -- but the select block
  * `VecQuickSort(pVec); solution = VecGet(pVec, k - 1);` (:32-33) becomes
- * VecKthSelect(pVec, k), i.e. the GPU selection through the C-ABI.
+ * VecKthSelectEx(pVec, k, &solution), i.e. the GPU selection through the
+ * C-ABI, with an explicit status instead of VecGet's in-band sentinels.
  *
  * Usage: kth_seq [n=100000000] [k=250] [seed=time(NULL)] [--median]
  *   --median sets k = n/2 as in kth-problem-seq.c~:24.
@@ -20,6 +21,7 @@
 #include <string.h>
 #include <time.h>
 
+#include "kth.h"
 #include "vector.h"
 
 int main(int argc, char **argv)
@@ -64,10 +66,17 @@ int main(int argc, char **argv)
     struct timespec w0, w1;
     clock_t start = clock();
     clock_gettime(CLOCK_MONOTONIC, &w0);
-    int solution = VecKthSelect(pVec, (int)k);
+    int solution = 0;
+    /* VecKthSelect keeps VecGet's in-band sentinels (a valid key could equal
+     * one); the driver takes the explicit status so a failure is loud */
+    const int rc = VecKthSelectEx(pVec, (int)k, &solution);
     clock_gettime(CLOCK_MONOTONIC, &w1);
     clock_t end = clock();
     VecDelete(pVec);
+    if (rc != 0) {
+        fprintf(stderr, "kth_seq: select failed: %s (no CPU fallback)\n", kth_strerror(rc));
+        return 1;
+    }
 
     double wall = (double)(w1.tv_sec - w0.tv_sec) + 1e-9 * (double)(w1.tv_nsec - w0.tv_nsec);
     printf("Solution found solution=%d \ntime: %f\n", solution, wall);

@@ -67,7 +67,8 @@ constexpr int MAX_EVENTS = 4 * 2048;
 
 struct kth_ctx {
     int device = 0;
-    int main_grid = 0;  // streaming-pass workgroups (num_cu * 8; KTH_MAIN_WG_PER_CU overrides)
+    int main_grid[3] = {0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
+    bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
@@ -340,11 +341,11 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.n_local = (u64)n;
     ev_main(c);
     if (tflag == 1)
-        kth::k_main<1><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+        kth::k_main<1><<<c->main_grid[1], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
     else if (tflag == 2)
-        kth::k_main<2><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+        kth::k_main<2><<<c->main_grid[2], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
     else
-        kth::k_main<0><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+        kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
     ev_main(c);
     // decide + candidate (or fallback) levels.  The grids cover the fallback
     // (whole input); in the common case only the WGs the candidates need run.
@@ -454,6 +455,7 @@ const char *kth_strerror(int code) {
     case KTH_EHIP: return "HIP runtime error";
     case KTH_ENODEV: return "no HIP device";
     case KTH_EINTERNAL: return "device-side consistency check failed";
+    case KTH_ECOMM: return "RCCL unavailable or a collective failed";
     default: return "unknown error";
     }
 }
@@ -492,27 +494,35 @@ int kth_ctx_create(int device, kth_ctx **out) {
             c->num_cu = prop.multiProcessorCount;
         {
             // One resident wave of workgroups: every WG streams an equal share
-            // and no tail of late WGs.  Residency from k_main's own VGPR and LDS
-            // use (4 waves per 256-thread WG = one per SIMD; a SIMD holds
-            // 512 / alloc(VGPR) waves, MI355X_MICROARCH.md register files).
+            // and no tail of late WGs.  Residency from each k_main variant's own
+            // VGPR and LDS use (4 waves per 256-thread WG = one per SIMD; a SIMD
+            // holds 512 / alloc(VGPR) waves, MI355X_MICROARCH.md register files);
+            // the top-k variants keep more keys live and may allocate more VGPRs.
             // hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports here.
-            int per = 4;
-            hipFuncAttributes fa;
-            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kth::k_main<0>)) == hipSuccess &&
-                fa.numRegs > 0) {
-                const int alloc = (fa.numRegs + 7) / 8 * 8;
-                const int by_vgpr = std::min(8, 512 / alloc);
-                const int lds = (int)fa.sharedSizeBytes;
-                const int by_lds = lds > 0 ? (160 * 1024) / lds : 8;
-                per = std::max(1, std::min(by_vgpr, by_lds));
-            }
-            (void)hipGetLastError();
+            const void *fns[3] = {reinterpret_cast<const void *>(kth::k_main<0>),
+                                  reinterpret_cast<const void *>(kth::k_main<1>),
+                                  reinterpret_cast<const void *>(kth::k_main<2>)};
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
-            if (e && atoi(e) > 0) per = atoi(e);
+            for (int v = 0; v < 3; ++v) {
+                int per = 4;
+                hipFuncAttributes fa;
+                if (hipFuncGetAttributes(&fa, fns[v]) == hipSuccess && fa.numRegs > 0) {
+                    const int alloc = (fa.numRegs + 7) / 8 * 8;
+                    const int by_vgpr = std::min(8, 512 / alloc);
+                    const int lds = (int)fa.sharedSizeBytes;
+                    const int by_lds = lds > 0 ? (160 * 1024) / lds : 8;
+                    per = std::max(1, std::min(by_vgpr, by_lds));
+                }
+                (void)hipGetLastError();
+                if (e && atoi(e) > 0) per = atoi(e);
+                c->main_grid[v] = c->num_cu * per;
+            }
             if (const char *g = getenv("KTH_SPARSE_PER_WG")) c->sparse_per_wg = (u64)std::max(0, atoi(g));
             if (const char *g = getenv("KTH_POST_DENSE_GRID")) c->post_dense_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
-            c->main_grid = c->num_cu * per;
+            // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
+            // so its count pass must report the bracket failure
+            c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
@@ -757,7 +767,9 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
     // tile flags from the streaming pass pay off when few 1024-key tiles can hold output
     const int tf = (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1) : 0;
-    KTH_TRY(select_async(c, d_keys, n, largest ? n - k + 1 : k, nullptr, c->d_status, tf, tflags));
+    int64_t rank = largest ? n - k + 1 : k;
+    if (c->fault_topk_rank && n > 1) rank = rank < n ? rank + 1 : rank - 1;
+    KTH_TRY(select_async(c, d_keys, n, rank, nullptr, c->d_status, tf, tflags));
     const uint32_t *keys = reinterpret_cast<const uint32_t *>(d_keys);
     const uint32_t flip = largest ? 0xFFFFFFFFu : 0u;
     u64 *toff = c->topk, *bsum = toff + ntiles, *bbase = bsum + 2 * nblk, *meta = bbase + 2 * nblk;
@@ -773,7 +785,10 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         kth::k_topk_count<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                      tflags, head, nfull);
     kth::k_topk_reduce<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, bsum);
-    kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta);
+    // a bracket failure (counts that do not hold the k-th) lands in the select's
+    // state, where kth_ctx_last_stats reports it as .error
+    kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta,
+                                                              c->st + c->last_state);
     kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
     if (aligned)
         kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
@@ -803,6 +818,10 @@ int kth_fill_synthetic(kth_ctx *c, int32_t *d_out, int64_t n, int64_t offset, in
 int64_t kth_dist_sample_size(int64_t n) { return sample_size(n); }
 
 int kth_sample_chunk(void) { return kth::SAMPLE_CHUNK; }
+
+double kth_window_z(void) { return window_z(); }
+
+int64_t kth_dist_cand_capacity(int64_t n_local) { return (int64_t)cand_capacity(std::max<int64_t>(n_local, 1)); }
 
 int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;
@@ -876,7 +895,7 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
-    kth::k_main<0><<<c->main_grid, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+    kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
     ev_main(c);
     c->dist_level_next = 0;
     KTH_TRY(launch_check());

@@ -571,6 +571,7 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 // {lo, hi, 1} (signed).  A row with no bit set in any wave holds no output key
 // of the top-k when its k-th lies inside the window.
 static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot in a byte");
+static_assert(BLK / WAVE == 4, "k_main<TF> stores one flag byte per wave, four per tile (tk_row_flagged's mask)");
 template <int TF>
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out,
                                               uint32_t *__restrict__ tflags) {

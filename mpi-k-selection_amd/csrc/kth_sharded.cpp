@@ -1,0 +1,325 @@
+// kth_sharded.cpp -- single-process multi-GPU selection (include/kth.h
+// kth_sharded_*, kth_select_i32_sharded).
+//
+// Replaces the whole CGM driver of the reference (TODO-kth-problem-cgm.c:81-278:
+// block partition + Scatterv, ~12 weighted-median rounds of Gather / Bcast /
+// Allreduce, final Gatherv + rank-0 sort) for a caller that holds one shard per
+// GPU in ONE process: the same per-rank device steps as the one-process-per-GPU
+// protocol (kth_dist_*), driven here for every device in turn, with the
+// collectives as grouped RCCL calls over communicators from ncclCommInitAll:
+//
+//   per device: begin, sample           -> ncclAllGather of the samples
+//   per device: window, scan            -> ncclAllReduce of the counts slot
+//   per device: level l (3 levels)      -> ncclAllReduce of the histogram slot
+//   per device: result                  -> every device holds the same answer
+//
+// Each device's work is enqueued on its own ctx stream, the collectives on the
+// same streams, so the host never waits between steps; it synchronises once at
+// the end to read the answer.  RCCL is resolved at first use (dlopen of the
+// librccl.so.1 already in the process, e.g. torch's, or the system one), so
+// libkth.so itself does not depend on it.
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kth.h"
+
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+};
+
+const Rccl &rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void *h = nullptr;
+        // prefer a copy already loaded (torch's), then the system one
+        const char *names[] = {"librccl.so.1", "librccl.so"};
+        for (const char *nm : names)
+            if (!h) h = dlopen(nm, RTLD_NOW | RTLD_NOLOAD);
+        const char *env = getenv("KTH_RCCL_LIB");
+        if (!h && env) h = dlopen(env, RTLD_NOW);
+        for (const char *nm : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+            if (!h) h = dlopen(nm, RTLD_NOW);
+        if (!h) return x;
+        x.CommInitAll = reinterpret_cast<decltype(x.CommInitAll)>(dlsym(h, "ncclCommInitAll"));
+        x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
+        x.AllReduce = reinterpret_cast<decltype(x.AllReduce)>(dlsym(h, "ncclAllReduce"));
+        x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
+        x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
+        x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
+        x.ok = x.CommInitAll && x.CommDestroy && x.AllReduce && x.AllGather && x.GroupStart && x.GroupEnd;
+        return x;
+    }();
+    return r;
+}
+
+#define TRY(x)                           \
+    do {                                 \
+        int r_ = (x);                    \
+        if (r_ < 0) return r_;           \
+    } while (0)
+#define HIPT(x)                                  \
+    do {                                         \
+        if ((x) != hipSuccess) {                 \
+            (void)hipGetLastError();             \
+            return KTH_EHIP;                     \
+        }                                        \
+    } while (0)
+#define NCCLT(x)                                 \
+    do {                                         \
+        if ((x) != ncclSuccess) return KTH_ECOMM; \
+    } while (0)
+
+constexpr int64_t SMALL_PER_GPU = 64;  // fewer keys on some GPU: gather to device 0
+
+struct Dev {
+    int device = 0;
+    kth_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    uint64_t *slots = nullptr;  // 3 * KTH_STATS_WORDS
+    uint32_t *sample = nullptr, *gathered = nullptr;
+    int64_t sample_cap = 0, gathered_cap = 0;
+    int32_t *out = nullptr;
+    int32_t *staging = nullptr;  // device 0: the union, small / unbalanced inputs
+    int64_t staging_cap = 0;
+};
+
+int grow(int device, void **p, int64_t *cap, int64_t bytes) {
+    if (*cap >= bytes) return KTH_OK;
+    HIPT(hipSetDevice(device));
+    HIPT(hipDeviceSynchronize());
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, (size_t)bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return KTH_ENOMEM;
+    }
+    *cap = bytes;
+    return KTH_OK;
+}
+
+}  // namespace
+
+struct kth_sharded {
+    std::vector<Dev> d;
+};
+
+namespace {
+
+// All shards copied next to each other on device 0, then one single-GPU select
+// (cf. the reference's final Gatherv + rank-0 solve, TODO-kth-problem-cgm.c:242-278).
+int select_gathered(kth_sharded *h, const int32_t *const *shards, const int64_t *shard_n, int64_t n_total, int64_t k,
+                    int32_t *out) {
+    Dev &d0 = h->d[0];
+    TRY(grow(d0.device, reinterpret_cast<void **>(&d0.staging), &d0.staging_cap, std::max<int64_t>(n_total, 1) * 4));
+    HIPT(hipSetDevice(d0.device));
+    for (Dev &x : h->d) HIPT(hipStreamSynchronize(x.stream));  // callers' earlier work on the shards
+    int64_t off = 0;
+    for (size_t i = 0; i < h->d.size(); ++i) {
+        if (shard_n[i] > 0)
+            HIPT(hipMemcpyPeerAsync(d0.staging + off, d0.device, shards[i], h->d[i].device, (size_t)shard_n[i] * 4,
+                                    d0.stream));
+        off += shard_n[i];
+    }
+    return kth_select_i32_ctx(d0.ctx, d0.staging, n_total, k, out);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kth_sharded_destroy(kth_sharded *h) {
+    if (!h) return KTH_EINVAL;
+    for (Dev &x : h->d) {
+        (void)hipSetDevice(x.device);
+        if (x.stream) (void)hipStreamSynchronize(x.stream);
+        if (x.comm && rccl().ok) (void)rccl().CommDestroy(x.comm);
+        if (x.slots) (void)hipFree(x.slots);
+        if (x.sample) (void)hipFree(x.sample);
+        if (x.gathered) (void)hipFree(x.gathered);
+        if (x.out) (void)hipFree(x.out);
+        if (x.staging) (void)hipFree(x.staging);
+        if (x.ctx) (void)kth_ctx_destroy(x.ctx);  // before its stream: it synchronises on it
+        if (x.stream) (void)hipStreamDestroy(x.stream);
+    }
+    delete h;
+    return KTH_OK;
+}
+
+int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
+    if (!out) return KTH_EINVAL;
+    *out = nullptr;
+    if (!devices || ngpu < 1) return KTH_EINVAL;
+    const int ndev = kth_device_count();
+    if (ndev <= 0) return KTH_ENODEV;
+    for (int i = 0; i < ngpu; ++i) {
+        if (devices[i] < 0 || devices[i] >= ndev) return KTH_EINVAL;
+        for (int j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) return KTH_EINVAL;  // RCCL needs one rank per device
+    }
+    if (!rccl().ok) return KTH_ECOMM;
+    kth_sharded *h = new kth_sharded();
+    h->d.resize((size_t)ngpu);
+    int rc = KTH_OK;
+    std::vector<ncclComm_t> comms((size_t)ngpu, nullptr);
+    for (int i = 0; i < ngpu && rc == KTH_OK; ++i) {
+        Dev &x = h->d[(size_t)i];
+        x.device = devices[i];
+        if ((rc = kth_ctx_create(x.device, &x.ctx)) != KTH_OK) break;
+        if (hipSetDevice(x.device) != hipSuccess ||
+            hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+            rc = KTH_EHIP;
+            break;
+        }
+        if ((rc = kth_ctx_set_stream(x.ctx, x.stream)) != KTH_OK) break;
+        if (hipMalloc(reinterpret_cast<void **>(&x.slots), 3 * (size_t)KTH_STATS_WORDS * 8) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&x.out), 4) != hipSuccess) {
+            rc = KTH_ENOMEM;
+            break;
+        }
+    }
+    if (rc == KTH_OK) {
+        if (rccl().CommInitAll(comms.data(), ngpu, devices) != ncclSuccess)
+            rc = KTH_ECOMM;
+        else
+            for (int i = 0; i < ngpu; ++i) h->d[(size_t)i].comm = comms[(size_t)i];
+    }
+    (void)hipGetLastError();
+    if (rc != KTH_OK) {
+        kth_sharded_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return KTH_OK;
+}
+
+int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const int64_t *shard_n, int64_t k,
+                           int32_t *out) {
+    if (!h || !shards || !shard_n || !out) return KTH_EINVAL;
+    const int P = (int)h->d.size();
+    int64_t n_total = 0, n_min = INT64_MAX;
+    for (int i = 0; i < P; ++i) {
+        if (shard_n[i] < 0 || (shard_n[i] > 0 && !shards[i])) return KTH_EINVAL;
+        n_total += shard_n[i];
+        n_min = std::min(n_min, shard_n[i]);
+    }
+    if (k < 1 || k > n_total) return KTH_EINVAL;
+    if (n_min < SMALL_PER_GPU) return select_gathered(h, shards, shard_n, n_total, k, out);
+
+    // ~kth_dist_sample_size(n_total) sample keys in all, split over the devices
+    // (as many per device: unbalanced shards only make the window a worse guess)
+    int64_t s = std::max<int64_t>(64, (kth_dist_sample_size(n_total) / P) & ~int64_t(63));
+    s = std::min<int64_t>(s, n_min & ~int64_t(63));
+    const Rccl &R = rccl();
+    for (Dev &x : h->d) {
+        TRY(grow(x.device, reinterpret_cast<void **>(&x.sample), &x.sample_cap, s * 4));
+        TRY(grow(x.device, reinterpret_cast<void **>(&x.gathered), &x.gathered_cap, s * 4 * P));
+    }
+    auto allreduce = [&](int slot) -> int {
+        NCCLT(R.GroupStart());
+        for (Dev &x : h->d) {
+            uint64_t *p = x.slots + (size_t)slot * KTH_STATS_WORDS;
+            if (R.AllReduce(p, p, KTH_STATS_WORDS, ncclUint64, ncclSum, x.comm, x.stream) != ncclSuccess) {
+                (void)R.GroupEnd();
+                return KTH_ECOMM;
+            }
+        }
+        NCCLT(R.GroupEnd());
+        return KTH_OK;
+    };
+    for (int i = 0; i < P; ++i) {
+        Dev &x = h->d[(size_t)i];
+        TRY(kth_dist_begin(x.ctx, x.slots, n_total, k));
+        TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], x.sample, s));
+    }
+    NCCLT(R.GroupStart());
+    for (Dev &x : h->d)
+        if (R.AllGather(x.sample, x.gathered, (size_t)s, ncclUint32, x.comm, x.stream) != ncclSuccess) {
+            (void)R.GroupEnd();
+            return KTH_ECOMM;
+        }
+    NCCLT(R.GroupEnd());
+    int slot = -1;
+    for (int i = 0; i < P; ++i) {
+        Dev &x = h->d[(size_t)i];
+        TRY(kth_dist_window(x.ctx, x.gathered, s * P));
+        const int r = kth_dist_scan(x.ctx, shards[i], shard_n[i]);
+        TRY(r);
+        slot = r;
+    }
+    TRY(allreduce(slot));
+    for (int l = 0; l < KTH_DIST_LEVELS; ++l) {
+        for (int i = 0; i < P; ++i) {
+            const int r = kth_dist_level(h->d[(size_t)i].ctx, shards[i], shard_n[i], l);
+            TRY(r);
+            slot = r;
+        }
+        TRY(allreduce(slot));
+    }
+    for (Dev &x : h->d) TRY(kth_dist_result(x.ctx, x.out));
+    // every device must hold the same answer (they picked the same digits from
+    // the same reduced histograms); the per-device error words must be clear
+    int32_t first = 0;
+    for (int i = 0; i < P; ++i) {
+        Dev &x = h->d[(size_t)i];
+        kth_stats st;
+        TRY(kth_ctx_last_stats(x.ctx, &st));  // synchronises x's stream
+        if (st.error != 0) return KTH_EINTERNAL;
+        int32_t a = 0;
+        HIPT(hipSetDevice(x.device));
+        HIPT(hipMemcpy(&a, x.out, 4, hipMemcpyDeviceToHost));
+        if (i == 0) first = a;
+        else if (a != first) return KTH_EINTERNAL;
+    }
+    *out = first;
+    return KTH_OK;
+}
+
+// One-shot form: shard i's device from its pointer; the handle (RCCL
+// communicators, per-device ctx and scratch) is kept per host thread and
+// reused while the device list stays the same.
+int kth_select_i32_sharded(const int32_t *const *dev_shards, const int64_t *shard_n, int ngpu, int64_t k,
+                           int32_t *out) {
+    static thread_local kth_sharded *cached = nullptr;
+    static thread_local std::vector<int> cached_devs;
+    if (!dev_shards || !shard_n || !out || ngpu < 1) return KTH_EINVAL;
+    if (kth_device_count() <= 0) return KTH_ENODEV;
+    std::vector<int> devs((size_t)ngpu);
+    for (int i = 0; i < ngpu; ++i) {
+        if (!dev_shards[i]) return KTH_EINVAL;
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, dev_shards[i]) != hipSuccess) {
+            (void)hipGetLastError();
+            return KTH_EINVAL;
+        }
+        if (at.type != hipMemoryTypeDevice) return KTH_EINVAL;  // device memory only
+        devs[(size_t)i] = at.device;
+    }
+    if (!cached || cached_devs != devs) {
+        if (cached) kth_sharded_destroy(cached);
+        cached = nullptr;
+        cached_devs.clear();
+        TRY(kth_sharded_create(devs.data(), ngpu, &cached));
+        cached_devs = devs;
+    }
+    return kth_sharded_select_i32(cached, dev_shards, shard_n, k, out);
+}
+
+}  // extern "C"

@@ -154,9 +154,13 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_reduce(const uint32_t *__rest
 
 // Pass 3: one workgroup: bbase[2b], bbase[2b+1] = exclusive prefixes of the
 // better / equal block sums; meta[0] = need = k - #better; meta[1] = error
-// when the counts do not bracket k (cannot happen for a correct v).
+// when the counts do not bracket k (cannot happen for a correct v).  The error
+// is also raised in the select's state (SelState.error = TK_ERR_BRACKET), which
+// kth_ctx_last_stats reports; k_topk_write then writes nothing.
+constexpr uint32_t TK_ERR_BRACKET = 32;
 __global__ __launch_bounds__(TK_SCAN_BLOCK) void k_topk_scan(const u64 *__restrict__ cnt, int G, u64 k,
-                                                             u64 *__restrict__ base, u64 *__restrict__ meta) {
+                                                             u64 *__restrict__ base, u64 *__restrict__ meta,
+                                                             SelState *__restrict__ st) {
     const int per = (G + TK_SCAN_BLOCK - 1) / TK_SCAN_BLOCK;
     const int g0 = threadIdx.x * per;
     u64 sb = 0, se = 0;
@@ -180,6 +184,7 @@ __global__ __launch_bounds__(TK_SCAN_BLOCK) void k_topk_scan(const u64 *__restri
         const bool ok = tb < k && k <= tb + te;
         meta[0] = ok ? k - tb : 0;
         meta[1] = ok ? 0 : 1;
+        if (!ok && st) st->error = TK_ERR_BRACKET;
     }
 }
 

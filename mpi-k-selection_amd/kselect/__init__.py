@@ -24,6 +24,7 @@ import numpy as np
 
 from ._lib import (  # noqa: F401
     KTH_DIST_LEVELS,
+    KTH_ECOMM,
     KTH_EINVAL,
     KTH_ENODEV,
     KTH_OK,
@@ -73,6 +74,10 @@ def _ptr(x):
     if isinstance(x, np.ndarray):
         return x.ctypes.data
     raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def _numel(x):
+    return x.numel() if hasattr(x, "numel") else len(x)
 
 
 def _stream_handle(stream):
@@ -198,6 +203,50 @@ def kth_select(keys, k):
         n = keys.numel()
     out = ctypes.c_int32()
     check(LIB.kth_select_i32(_ptr(keys), int(n), int(k), ctypes.byref(out)), "kth_select_i32")
+    return out.value
+
+
+class ShardedSelector:
+    """One process, several GPUs (kth_sharded_*): shard i lives on devices[i];
+    the union's k-th smallest through grouped RCCL collectives
+    (replaces TODO-kth-problem-cgm.c:81-278 without one process per rank)."""
+
+    def __init__(self, devices):
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        self._h = ctypes.c_void_p()
+        check(LIB.kth_sharded_create(arr, len(self.devices), ctypes.byref(self._h)), "kth_sharded_create")
+
+    def select(self, shards, k, sizes=None):
+        """shards: one device tensor per device (int32); sizes default to numel()."""
+        if len(shards) != len(self.devices):
+            raise ValueError(f"{len(shards)} shards for {len(self.devices)} devices")
+        sizes = [_numel(s) for s in shards] if sizes is None else [int(x) for x in sizes]
+        ptrs = (ctypes.c_void_p * len(shards))(*[_ptr(s) for s in shards])
+        ns = (ctypes.c_int64 * len(shards))(*sizes)
+        out = ctypes.c_int32()
+        check(LIB.kth_sharded_select_i32(self._h, ptrs, ns, int(k), ctypes.byref(out)), "kth_sharded_select_i32")
+        return out.value
+
+    def close(self):
+        if self._h:
+            LIB.kth_sharded_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def select_sharded(shards, k, sizes=None):
+    """One-shot kth_select_i32_sharded: each shard's device from its pointer."""
+    sizes = [_numel(s) for s in shards] if sizes is None else [int(x) for x in sizes]
+    ptrs = (ctypes.c_void_p * len(shards))(*[_ptr(s) for s in shards])
+    ns = (ctypes.c_int64 * len(shards))(*sizes)
+    out = ctypes.c_int32()
+    check(LIB.kth_select_i32_sharded(ptrs, ns, len(shards), int(k), ctypes.byref(out)), "kth_select_i32_sharded")
     return out.value
 
 

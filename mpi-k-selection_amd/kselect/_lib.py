@@ -17,6 +17,7 @@ KTH_ENOMEM = -2
 KTH_EHIP = -3
 KTH_ENODEV = -4
 KTH_EINTERNAL = -5
+KTH_ECOMM = -6
 
 KTH_PATH_LDS, KTH_PATH_RADIX, KTH_PATH_WINDOW, KTH_PATH_WINDOW_FALLBACK = 1, 2, 3, 4
 KTH_STATS_WORDS = 8 + 2 * 2048
@@ -103,6 +104,12 @@ PROTOS = {
     "kth_dist_result": (ctypes.c_int, [c_vp, c_vp]),
     "kth_dist_sample_size": (ctypes.c_int64, [ctypes.c_int64]),
     "kth_sample_chunk": (ctypes.c_int, []),
+    "kth_window_z": (ctypes.c_double, []),
+    "kth_dist_cand_capacity": (ctypes.c_int64, [ctypes.c_int64]),
+    "kth_sharded_create": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "kth_sharded_destroy": (ctypes.c_int, [c_vp]),
+    "kth_sharded_select_i32": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_i32p]),
+    "kth_select_i32_sharded": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int64, c_i32p]),
     # vector.h
     "VecNew": (IntVectorPtr, [ctypes.c_int]),
     "VecAdd": (ctypes.c_int, [IntVectorPtr, ctypes.c_int]),

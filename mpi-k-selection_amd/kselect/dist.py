@@ -115,6 +115,7 @@ class DistSelector:
         self.out = backend.alloc_out()
         self._sample = None
         self._gathered = None
+        self._checked = None  # last (n_local, n_total, k) every rank agreed on
 
     def select(self, shard, n_local, n_total, k, out=None):
         """Enqueue one selection; returns the device (or CPU, for gloo) int32[1]
@@ -125,18 +126,17 @@ class DistSelector:
         balanced (every n_local >= n_total // world, as the block partition of
         shard_bounds gives); below SMALL_PER_RANK keys per rank the shards are
         all-gathered and every rank selects from the union."""
-        if not (1 <= k <= n_total):
-            raise ValueError(f"k={k} outside [1, {n_total}]")
         b = self.b
         out = self.out if out is None else out
         if n_total // self.world < SMALL_PER_RANK:
+            if not (1 <= k <= n_total):
+                raise ValueError(f"k={k} outside [1, {n_total}]")
             return self._select_small(shard, n_local, n_total, k, out)
         # the window needs ~sample_size(n_total) sample keys in all (what one GPU
         # would take), not that many per rank: the all-gather stays ~4 MiB
         s_local = max(64, (b.sample_size(n_total) // self.world) & ~63)
-        if n_local < s_local:
-            raise ValueError(f"shard of {n_local} keys is smaller than the per-rank sample ({s_local}); "
-                             "use balanced shards (kselect.dist.shard_bounds)")
+        if self._checked != (n_local, n_total, k):
+            self._check_args(n_local, n_total, k, s_local)
         if self._sample is None or self._sample.numel() != s_local:
             self._sample = b.alloc_sample(s_local)
             self._gathered = b.alloc_sample(s_local * self.world)
@@ -151,6 +151,28 @@ class DistSelector:
             self.comm.all_reduce_sum_(self.slots[i])
         b.result(out)
         return out
+
+    def _check_args(self, n_local, n_total, k, s_local):
+        """Validate the arguments across ranks (two small collectives, once per
+        distinct (n_local, n_total, k)), so that every rank raises together
+        instead of one rank raising while the others wait in a collective."""
+        dev = self.out.device
+        mx = torch.tensor([n_total, -n_total, k, -k, 0 if n_local >= s_local else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
+        tot = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=self.group)
+        mx, tot = mx.tolist(), int(tot.item())
+        if mx[0] != -mx[1] or mx[2] != -mx[3]:
+            raise ValueError(f"ranks disagree on n_total / k (n_total in [{-mx[1]}, {mx[0]}], "
+                             f"k in [{-mx[3]}, {mx[2]}])")
+        if tot != n_total:
+            raise ValueError(f"shard sizes sum to {tot}, not n_total={n_total}")
+        if not (1 <= k <= n_total):
+            raise ValueError(f"k={k} outside [1, {n_total}]")
+        if mx[4]:
+            raise ValueError(f"some shard is smaller than the per-rank sample ({s_local} keys); "
+                             "use balanced shards (kselect.dist.shard_bounds)")
+        self._checked = (n_local, n_total, k)
 
     def _select_small(self, shard, n_local, n_total, k, out):
         """Tiny inputs (cf. the reference's final Gatherv + solve on one rank,

@@ -3,28 +3,34 @@
 
 TEST INFRASTRUCTURE ONLY: lets tests/test_dist_gloo.py run the product's
 orchestration (kselect.dist.DistSelector) on gloo with world_size > 1 on CPU.
-The slot layout, window ranks, decide and digit-pick rules mirror the device
-code exactly (same constants, same arithmetic), so the all-reduced slots carry
-the same numbers a GPU run would.
+The slot layout, window ranks, decide and digit-pick rules restate the device
+code, and the tunable constants (sample size and chunk layout, window z,
+candidate capacity) are read from libkth.so itself (kth_dist_sample_size,
+kth_sample_chunk, kth_window_z, kth_dist_cand_capacity; no GPU needed), so the
+all-reduced slots carry the same numbers a GPU run does --
+tests/test_gpu_parity.py::test_dist_backend_slots_match checks that slot by slot.
 """
 import math
 
 import numpy as np
 import torch
 
+from kselect import LIB
+
 NCOUNTS, DIGIT, NBINS = 8, 11, 2048
 STATS_WORDS = NCOUNTS + 2 * NBINS
 C_LT, C_EQLO, C_EQHI, C_IN, C_OVF = range(5)
-SAMPLE_MAX, WINDOW_Z = 1 << 20, 6.0
 MAIN, CAND, FULL, DONE = "main", "cand", "full", "done"
+WINDOW_Z = float(LIB.kth_window_z())
+SAMPLE_CHUNK = int(LIB.kth_sample_chunk())
 
 
 def sample_size(n_local):
-    s = (n_local // 64) & ~63
-    return min(SAMPLE_MAX, max(s, 64))
+    return int(LIB.kth_dist_sample_size(int(n_local)))
 
 
 def window_ranks(n, k, s):
+    """kth_api.hip window_ranks: +-(z sigma + 2) around p*s, p = k/n."""
     p = k / n
     r = p * s
     sig = math.sqrt(max(1.0, s * p * (1.0 - p)))
@@ -36,7 +42,18 @@ def window_ranks(n, k, s):
 
 
 def cand_capacity(n):
-    return max(1 << 20, n // 32)
+    return int(LIB.kth_dist_cand_capacity(int(n)))
+
+
+def sample_indices(n_local, s_local):
+    """k_gather's layout (include/kth.h kth_sample_chunk): ceil(s/C) chunks of
+    C consecutive keys, chunk c at key c * (n / ceil(s/C)); the last chunk holds
+    the remaining s mod C keys.  Indices past the shard read as order key 0."""
+    C = SAMPLE_CHUNK
+    nch = (s_local + C - 1) // C
+    stride = n_local // nch
+    idx = (np.arange(nch, dtype=np.int64)[:, None] * stride + np.arange(C, dtype=np.int64)[None, :]).ravel()
+    return idx[:s_local]
 
 
 class CpuBackend:
@@ -67,10 +84,10 @@ class CpuBackend:
         self.mode = None
 
     def sample(self, shard, n_local, out, s_local):
-        nch = s_local // 64
-        stride = n_local // nch
-        idx = (np.arange(nch, dtype=np.int64)[:, None] * stride + np.arange(64)[None, :]).ravel()
-        keys = shard.numpy()[idx].view(np.uint32) ^ np.uint32(0x80000000)
+        idx = sample_indices(n_local, s_local)
+        ok = idx < n_local
+        keys = np.zeros(s_local, dtype=np.uint32)
+        keys[ok] = shard.numpy()[idx[ok]].view(np.uint32) ^ np.uint32(0x80000000)
         out.numpy()[:] = keys.view(np.int32)
 
     def window(self, sample_all, s_total):

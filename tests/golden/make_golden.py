@@ -14,7 +14,11 @@ oracle/build_ref.sh compiles from it into oracle/_ref/).  Writes:
   and a "shipped" section: the unmodified reference programs run as shipped
   (n = 1e8), seeded through the --wrap=time shim, with their printed answers.
 
-Usage: python tests/golden/make_golden.py [--small] [--shipped]
+  and a "large" section: n in {16385, 2^20, 2^22 + 1} (radix and window paths,
+  BASELINE config 1), inputs regenerated from (family, seed, n) and pinned by
+  sha256, expected outputs from the reference seq block and mpirun CGM.
+
+Usage: python tests/golden/make_golden.py [--small] [--shipped] [--large]
 """
 import argparse
 import ctypes
@@ -134,6 +138,41 @@ def livelock_cases(lib):
     return out
 
 
+LARGE_NS = [16385, 1 << 20, (1 << 22) + 1]  # radix path (n > 16384), BASELINE config 1, window path (n > 4 Mi)
+LARGE_PS = [2, 8]
+
+
+def large(lib):
+    """Radix- and window-path sizes.  Inputs are NOT stored: each is the
+    counter-based generator's output for (family, seed, param, n) -- gen.py,
+    bit-identical to oracle ko_gen and the device's kth_fill_synthetic -- pinned
+    by its sha256; the reference seq select block and the reference CGM under
+    mpirun (P in LARGE_PS) give the expected outputs."""
+    tmp = tempfile.mkdtemp(prefix="ko_large_")
+    out = []
+    for name, dist, param in FAMILIES:
+        if name in ("all_equal_min", "all_equal_max"):
+            continue
+        for n in LARGE_NS:
+            a = G.gen(n, dist, G.DEFAULT_SEED, param)
+            path = os.path.join(tmp, "in.bin")
+            a.astype("<i4").tofile(path)
+            srt = np.sort(a.astype(np.int64))
+            for k in sorted({1, n // 2, n}):
+                case = {"family": name, "dist": dist, "param": param, "seed": G.DEFAULT_SEED, "n": n, "k": k,
+                        "input_sha256": sha256_file(path), "true": int(srt[k - 1]),
+                        "seq_ref": seq_ref(lib, a, k), "cgm_ref": {}}
+                env = dict(os.environ, KO_N=str(n), KO_K=str(k), KO_TIME="1", KO_INPUT=path)
+                for P in LARGE_PS:
+                    case["cgm_ref"][str(P)], _ = run_cgm(os.path.join(REF_DIR, "cgm_param"), P, env, 10.0)
+                case["seq_ref_defect"] = case["seq_ref"] != case["true"]
+                out.append(case)
+                print("large", name, n, k, case["true"], case["seq_ref"], case["cgm_ref"], flush=True)
+            os.remove(path)
+    os.rmdir(tmp)
+    return out
+
+
 def sha256_file(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -199,9 +238,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--shipped", action="store_true")
+    ap.add_argument("--large", action="store_true")
     args = ap.parse_args()
-    if not (args.small or args.shipped):
-        args.small = args.shipped = True
+    if not (args.small or args.shipped or args.large):
+        args.small = args.shipped = args.large = True
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     lib = ctypes.CDLL(os.path.join(REF_DIR, "libvector_ref.so"))
     lib.VecGet.restype = ctypes.c_int
@@ -213,6 +253,8 @@ def main():
         doc["cases"] = small(lib) + livelock_cases(lib)
     if args.shipped:
         doc["shipped"] = shipped()
+    if args.large:
+        doc["large"] = large(lib)
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
     print("wrote", path)

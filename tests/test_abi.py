@@ -171,3 +171,44 @@ def test_reference_driver_links_against_twin(tmp_path):
     subprocess.run(["gcc", "-O2", "-w", "-I", os.path.join(REPO, "include"), src, "-L", os.path.dirname(LIB),
                     "-lkth", "-o", str(exe)], check=True)
     assert exe.exists()
+
+
+def test_sharded_argument_checks(lib):
+    """kth_select_i32_sharded / kth_sharded_*: bad arguments are EINVAL before
+    any device work; without a GPU the compute entry points are ENODEV."""
+    import torch
+    import kselect
+    a = np.arange(1000, dtype=np.int32)
+    ptrs = (ctypes.c_void_p * 1)(a.ctypes.data)
+    ns = (ctypes.c_int64 * 1)(1000)
+    out = ctypes.c_int32(99)
+    assert lib.kth_select_i32_sharded(None, ns, 1, 5, ctypes.byref(out)) == kselect.KTH_EINVAL
+    assert lib.kth_select_i32_sharded(ptrs, None, 1, 5, ctypes.byref(out)) == kselect.KTH_EINVAL
+    assert lib.kth_select_i32_sharded(ptrs, ns, 0, 5, ctypes.byref(out)) == kselect.KTH_EINVAL
+    assert lib.kth_select_i32_sharded(ptrs, ns, 1, 5, None) == kselect.KTH_EINVAL
+    h = ctypes.c_void_p()
+    assert lib.kth_sharded_create(None, 1, ctypes.byref(h)) == kselect.KTH_EINVAL
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.kth_sharded_create(devs, 0, ctypes.byref(h)) == kselect.KTH_EINVAL
+    assert lib.kth_sharded_select_i32(None, ptrs, ns, 5, ctypes.byref(out)) == kselect.KTH_EINVAL
+    assert lib.kth_sharded_destroy(None) == kselect.KTH_EINVAL
+    if not torch.cuda.is_available():
+        assert lib.kth_select_i32_sharded(ptrs, ns, 1, 5, ctypes.byref(out)) == kselect.KTH_ENODEV
+        assert lib.kth_sharded_create(devs, 1, ctypes.byref(h)) == kselect.KTH_ENODEV
+        assert out.value == 99
+    assert lib.kth_strerror(kselect.KTH_ECOMM).decode().startswith("RCCL")
+
+
+def test_protocol_constants_exported(lib):
+    """The tunables the gloo CPU backend mirrors are read from the library
+    (tests/dist_cpu_backend.py), not restated: window z, sample chunk and
+    size rule, candidate capacity."""
+    import dist_cpu_backend as cb
+    assert lib.kth_window_z() == 5.0 == cb.WINDOW_Z
+    assert lib.kth_sample_chunk() == 1024 == cb.SAMPLE_CHUNK
+    assert lib.kth_dist_sample_size(1 << 30) == 1 << 20
+    assert lib.kth_dist_sample_size(100) == 64
+    assert lib.kth_dist_cand_capacity(1 << 30) == (1 << 30) // 32
+    assert lib.kth_dist_cand_capacity(1000) == 1 << 20
+    idx = cb.sample_indices(1 << 24, (1 << 18) + 64)  # 257 chunks, the last one partial
+    assert idx.size == (1 << 18) + 64 and idx[1024] == (1 << 24) // 257 and idx[-1] == 256 * ((1 << 24) // 257) + 63

@@ -115,3 +115,52 @@ def test_dist_selector_gloo_fallback():
             assert got == int(srt[kk - 1]), (k, got)
     paths = {m for r in range(2) for *_, m in res[r]}
     assert paths == {"fallback"}
+
+
+def _bad_worker(rank, world, port, q):
+    sys.path.insert(0, HERE)
+    from conftest import PKG  # noqa: F401
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from dist_cpu_backend import CpuBackend
+    from kselect.dist import DistSelector
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ds = DistSelector(CpuBackend())
+        errs = []
+        n = 400_000
+        # rank 1 holds a shard smaller than its sample share: every rank must
+        # raise together (no rank left waiting in a collective)
+        sizes = [n - 100, 100]
+        shard = torch.arange(sizes[rank], dtype=torch.int32)
+        for args in ((shard, sizes[rank], n, n // 2),                        # unbalanced
+                     (shard, sizes[rank], n + rank, n // 2),                 # n_total disagrees
+                     (torch.arange(n // 2, dtype=torch.int32), n // 2, n + 5, 7)):  # sizes do not sum
+            try:
+                ds.select(*args)
+                errs.append(None)
+            except ValueError as e:
+                errs.append(str(e)[:40])
+        q.put((rank, errs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_selector_bad_arguments_raise_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert all(e is not None for e in res[r]), res
+    assert res[0] == res[1]

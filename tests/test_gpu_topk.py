@@ -128,3 +128,54 @@ def test_topk_window_path_unaligned_small_k(gpu):
                 want = _ref_idx(h, k, largest)
                 np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"off={off} k={k} {largest}")
                 np.testing.assert_array_equal(vals.cpu().numpy(), h[want])
+
+
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_tile_flag_cutoff_and_window_miss(gpu, largest):
+    """k = n // 1024 (streaming-pass tile flags on) and n // 1024 + 1 (off), and
+    inputs whose sample window misses the k-th (a spike of one value at the
+    median and a narrow band: the flags are not trusted, skip_ok false) or
+    whose candidates overflow (fallback levels)."""
+    import torch
+    n = (1 << 23) + 1029
+    rng = np.random.default_rng(23 + largest)
+    spike = rng.integers(-2 ** 31, 2 ** 31, size=n, dtype=np.int64).astype(np.int32)
+    spike[rng.random(n) < 0.3] = 12345
+    narrow = rng.integers(-2048, 2048, size=n).astype(np.int32)
+    uni = rng.integers(-2 ** 31, 2 ** 31, size=n, dtype=np.int64).astype(np.int32)
+    for name, a in (("uniform", uni), ("spike", spike), ("narrow", narrow)):
+        d = torch.from_numpy(a).cuda()
+        for k in (n // 1024, n // 1024 + 1, 1, n // 2):
+            vals, idx = _run(gpu, d, n, k, largest)
+            want = _ref_idx(a, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k}")
+            np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{name} k={k}")
+            assert gpu.stats()["error"] == 0
+
+
+def test_topk_bracket_failure_is_reported(gpu):
+    """A k-th that does not bracket k in the count pass (forced here with the
+    test-only KTH_FAULT_TOPK_RANK hook, which selects a neighbouring rank) must
+    surface as kth_ctx_last_stats().error and leave the outputs unwritten."""
+    import os
+    import torch
+    import kselect
+    os.environ["KTH_FAULT_TOPK_RANK"] = "1"
+    try:
+        faulty = kselect.Selector(0)  # the hook is read when a ctx is created
+    finally:
+        del os.environ["KTH_FAULT_TOPK_RANK"]
+    n, k = (1 << 22) + 7, 1000
+    a = np.random.default_rng(5).permutation(n).astype(np.int32)  # distinct keys
+    d = torch.from_numpy(a).cuda()
+    for largest in (False, True):
+        vals = torch.full((k,), -77, dtype=torch.int32, device="cuda")
+        idx = torch.full((k,), -77, dtype=torch.int64, device="cuda")
+        faulty.topk(d, n, k, vals, idx, largest=largest)
+        faulty.sync()
+        assert faulty.stats()["error"] == 32
+        assert bool((vals == -77).all()) and bool((idx == -77).all())
+    faulty.close()
+    vals, idx = _run(gpu, d, n, k, False)  # a normal ctx: no error
+    assert gpu.stats()["error"] == 0
+    np.testing.assert_array_equal(idx.cpu().numpy(), _ref_idx(a, k, False))

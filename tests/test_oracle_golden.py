@@ -111,3 +111,33 @@ def test_shipped_generators_and_answers(golden, oracle):
             assert oracle.ko_cgm_ref(a.ctypes.data, a.size, rec["k"], rec["P"], 500, ctypes.byref(out),
                                      ctypes.byref(r), ctypes.byref(f)) == 0
             assert out.value == rec["printed"], rec
+
+
+def test_large_fixtures_pin_the_restatement(golden, oracle):
+    """The radix/window-size fixtures (n in {16385, 2^20, 2^22 + 1}): the
+    generator reproduces each input (sha256), and the restated seq and CGM
+    reproduce the reference's answers, livelocks included."""
+    large = golden.get("large")
+    if not large:
+        pytest.skip("no large fixtures")
+    inputs = {}
+    mismatches = []
+    for c in large:
+        key = (c["dist"], c["param"], c["n"])
+        if key not in inputs:
+            a = G.gen(c["n"], c["dist"], c["seed"], c["param"])
+            assert hashlib.sha256(a.astype("<i4").tobytes()).hexdigest() == c["input_sha256"], c
+            inputs = {key: a}
+        a = inputs[key]
+        assert true_kth(oracle, a, c["k"]) == c["true"], c
+        if c["n"] <= 1 << 20:  # qsort of 4 Mi keys per case is slow for the CPU suite
+            assert oracle.ko_seq_ref(a.ctypes.data, a.size, c["k"]) == c["seq_ref"], c
+        for p, ref in c["cgm_ref"].items():
+            out, rounds, found = ctypes.c_int32(), ctypes.c_int(), ctypes.c_int()
+            st = oracle.ko_cgm_ref(a.ctypes.data, a.size, c["k"], int(p), 500, ctypes.byref(out),
+                                   ctypes.byref(rounds), ctypes.byref(found))
+            if (ref == "livelock" and st != 1) or (ref != "livelock" and (st != 0 or out.value != ref)):
+                mismatches.append((c["family"], c["n"], c["k"], p, ref, st, out.value))
+    assert not mismatches, mismatches[:10]
+    assert any(c["seq_ref_defect"] for c in large) and any(v == "livelock" for c in large
+                                                          for v in c["cgm_ref"].values())
