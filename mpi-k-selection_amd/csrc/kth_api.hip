@@ -192,6 +192,29 @@ void dump_stamps(kth_ctx *c) {
             if (cnt) fprintf(stderr, " p%d %6.2f/%6.2f", i, sum / cnt, mx);
         }
         fprintf(stderr, "\n");
+        if (nwg >= 512) {  // end times (p5): percentiles over workgroups, and per blockIdx % 8
+            std::vector<double> e;
+            std::vector<double> ex[8];
+            for (int w = 0; w < STAMP_WGS; ++w)
+                if (b[w * 8] && b[w * 8 + 5]) {
+                    const double d = (b[w * 8 + 5] - t0) / 100.0;
+                    e.push_back(d);
+                    ex[w % 8].push_back(d);
+                }
+            std::sort(e.begin(), e.end());
+            if (!e.empty()) {
+                auto pc = [&](double q) { return e[std::min(e.size() - 1, (size_t)(q * (double)e.size()))]; };
+                fprintf(stderr, "kth-stamps   p5 pct: 1%% %.1f 10%% %.1f 25%% %.1f 50%% %.1f 75%% %.1f 90%% %.1f 99%% %.1f max %.1f\n",
+                        pc(0.01), pc(0.10), pc(0.25), pc(0.50), pc(0.75), pc(0.90), pc(0.99), e.back());
+                fprintf(stderr, "kth-stamps   p5 mean by wg%%8:");
+                for (int x = 0; x < 8; ++x) {
+                    double sm = 0;
+                    for (double d : ex[x]) sm += d;
+                    fprintf(stderr, " %.1f", ex[x].empty() ? 0.0 : sm / ex[x].size());
+                }
+                fprintf(stderr, "\n");
+            }
+        }
         if (nwg >= 512) {  // streaming pass: finish times (p3) by blockIdx % 8 (XCD under round-robin dispatch)
             for (int x = 0; x < 8; ++x) {
                 double sum = 0, mn = 1e30, mx = 0;

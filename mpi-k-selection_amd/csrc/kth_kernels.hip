@@ -582,6 +582,24 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     __shared__ uint32_t region[BLK / WAVE][WREG];
     __shared__ u64 red[6][BLK / WAVE];
     KTH_STAMP(a, 0);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(a.keys);
+    const u64 n = a.n_local;
+    u64 head = ((16u - (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u)) & 15u) >> 2;
+    if (head > n) head = n;
+    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(p + head);
+    const u64 nv = (n - head) >> 2, tail0 = head + (nv << 2);
+    const u64 tile = (u64)BLK * U, nfull = nv / tile;
+    // Full tiles are dealt grid-strided.  (Workgroups on every other XCD finish
+    // ~5 % later; handing the last 25 % of the tiles out dynamically per XCD
+    // evened the finish times but not the pass time: it is HBM-bound, and the
+    // early finishers' bandwidth goes to the rest.  DESIGN.md.)
+    auto load_tile = [&](uint4 (&x)[U], u64 t) {
+        const uint4 *src = v + t * tile + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
+    };
+    // (Issuing the first tile's loads before the advance made the pass slower,
+    // 656 vs 642 us: the advance's histogram loads then wait behind them.)
     advance<BLK>(ss, a, scratch);
     publish<BLK>(ss, 0, a);
     KTH_STAMP(a, 1);
@@ -598,19 +616,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     Stager st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
 
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(a.keys);
-    const u64 n = a.n_local;
-    u64 head = ((16u - (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u)) & 15u) >> 2;
-    if (head > n) head = n;
-    const uint4 *__restrict__ v = reinterpret_cast<const uint4 *>(p + head);
-    const u64 nv = (n - head) >> 2, tail0 = head + (nv << 2);
-    const u64 tile = (u64)BLK * U, nfull = nv / tile;
-    // full tiles: grid-strided; the tile is consumed in groups of 4 * MAIN_SUB keys
-    auto load_tile = [&](uint4 (&x)[U], u64 t) {
-        const uint4 *src = v + t * tile + threadIdx.x;
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
-    };
+    // a tile is consumed in groups of 4 * MAIN_SUB keys
     auto scan_tile = [&](const uint4 (&x)[U]) {
 #pragma unroll
         for (int h = 0; h < U / S; ++h) {
@@ -625,11 +631,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             scan_keys<K, true>(kk, 0xFFFFFFFFu, slo, shi, clt, ceqlo, ceqhi, st);
         }
     };
-    // every load of a tile issued before any use
-    for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
-        uint4 x[U];
-        load_tile(x, t);
-        scan_tile(x);
+    auto flag_tile = [&](const uint4 (&x)[U], u64 t) {
         if constexpr (TF != 0) {
             // bit u of the wave's byte: some key of row u (the tile's u-th run of
             // 4 * BLK keys) in this wave's part is <= hi (TF 1) / >= lo (TF 2)
@@ -642,6 +644,13 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             }
             if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = (uint8_t)rows;
         }
+    };
+    // every load of a tile issued before any use
+    for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
+        uint4 x[U];
+        load_tile(x, t);
+        scan_tile(x);
+        flag_tile(x, t);
     }
     // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;
