@@ -25,6 +25,9 @@ constexpr int RW_BLOCK = 256;
 #define KTH_TOPK_RELOAD 1
 #endif
 constexpr bool TOPK_RELOAD = KTH_TOPK_RELOAD;  // top-k compaction re-reads full rows from L2
+#ifndef KTH_TOPK_NT
+#define KTH_TOPK_NT 1  // top-k rows load with the non-temporal hint too (the staged path reads a row once)
+#endif
 #ifndef KTH_ROWS_WAVES
 #define KTH_ROWS_WAVES 4  // waves per SIMD the register budget is held to (<= 128 VGPRs)
 #endif
@@ -351,20 +354,36 @@ __device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
 //       bin LINEAR IN THE VALUE over (about) the row's own [vmin, vmax]
 //       (vbin), so uniform floats fill the bins evenly instead of piling onto
 //       a few exponent bytes.  Float keys stay raw bits until they are needed
-//       as order keys;
-//   filter: the keys of the picked bin B (same b, recomputed) are appended to
-//       the wave's LDS list (ballot + mbcnt, only on the slots where some lane
-//       has one);
+//       as order keys; their value bins are kept, four to a register, for the
+//       filter (no second fma / clamp per key);
+//   filter: the keys of the picked bin B are appended to the wave's LDS list
+//       (ballot + mbcnt, only on the slots where some lane has one);
 //   rank: with L <= 64 listed keys, lane i ranks list[i] against the list.
 // b is monotone, so the bin's keys are exactly the keys between two order
 // keys, and the kk-th of the row is the kk-th (after the keys below B) of the
 // list.  A bin of more than 64 keys (duplicate-heavy or clustered rows) goes
-// to the masked radix sweeps of row_select_radix.  Per key: ~5 VALU ops
-// (int32) / ~11 (float) and one LDS atomic.  On return key[] holds order keys
-// (xor flip) when KEYS_OUT (top-k compaction); else float rows may keep raw bits.
-template <bool F32, int KPL, int R0, bool KEYS_OUT>
+// to the masked radix sweeps of row_select_radix.  On return key[] holds order
+// keys (xor flip) when KEYS_OUT (top-k compaction); else float rows may keep
+// raw bits.  *eq_out: how many keys of the row equal the answer.
+// Top-k rows (STAGE): the filter pass also stages every key of the bins up to
+// B -- all the kept keys and the rest of bin B -- as (value, column) pairs in
+// column order, and after the rank step one ordered compaction of those pairs
+// writes the row's top-k (*topk_done = true).  No second look at the row.  The
+// pairs need 2 * (below + cnt) words after the list; rows whose bins do not fit,
+// or whose bin B is too full for the list, leave *topk_done false for the
+// caller's general compaction.
+struct TopkOut {
+    uint32_t k;
+    uint32_t *vals;
+    int32_t *idx;
+    u64 obase;
+};
+constexpr int STAGE_OFF = WAVE;  // staged pairs start after the list's 64 words
+
+template <bool F32, int KPL, int R0, bool KEYS_OUT, bool STAGE = false>
 __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
-                                                    uint32_t flip) {
+                                                    uint32_t flip, uint32_t *eq_out = nullptr,
+                                                    const TopkOut *tko = nullptr, bool *topk_done = nullptr) {
     auto to_keys = [&]() {
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {
@@ -372,26 +391,26 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             key[j] = key_of_f32(key[j]) ^ flip;
         }
     };
-    bool fmap = false;
+    bool vmap = false;  // wave-uniform: value-linear bins (F32 rows without NaN)
     float fs = 0.f, fo = 0.f;
-    if (F32) {  // key[] holds raw float bits
+    if constexpr (F32) {  // key[] holds raw float bits
         // The bin map's range comes from every 4th key: keys outside it clamp
         // into the end bins, which stays monotone (and exact), so the range only
         // has to be close.  Infinities clamp the same way.  NaNs (last in the
-        // order) would not, so every key is checked for one.
+        // order) would not, so every key is tested for one: an unordered compare
+        // of two keys per instruction, straight into a wave mask.
         float vmin = __uint_as_float(key[0]), vmax = vmin;
-        bool nan = false;
+        unsigned long long nanm = 0;
 #pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const float a = __uint_as_float(key[j]);
-            nan |= a != a;
+        for (int j = 0; j < KPL; j += 2) {
+            const float a = __uint_as_float(key[j]), b = __uint_as_float(key[j + 1]);
+            nanm |= __builtin_amdgcn_ballot_w64(a != a || b != b);
             if (j % 8 == 4) {
-                const float b = __uint_as_float(key[j - 4]);
-                vmin = min3f(vmin, a, b);
-                vmax = max3f(vmax, a, b);
+                const float c = __uint_as_float(key[j - 4]);
+                vmin = min3f(vmin, a, c);
+                vmax = max3f(vmax, a, c);
             }
         }
-        const bool anynan = __ballot(nan) != 0;
         vmin = __uint_as_float(wave_reduce(__float_as_uint(vmin), 0x7F800000u, [](uint32_t a, uint32_t b) {
             return __float_as_uint(min3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
         }));
@@ -399,19 +418,19 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             return __float_as_uint(max3f(__uint_as_float(a), __uint_as_float(b), __uint_as_float(b)));
         }));
         const float range = vmax - vmin, scale = 256.0f / range;
-        fmap = !anynan && __builtin_isfinite(range) && range > 0.f && __builtin_isfinite(scale) && scale > 0.f;
+        vmap = nanm == 0 && __builtin_isfinite(range) && range > 0.f && __builtin_isfinite(scale) && scale > 0.f;
         // bins ascend with the selection order: ascending v (flip = 0) or descending
         fs = flip ? -scale : scale;
         fo = flip ? vmax * scale : -vmin * scale;
         fs = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fs)));
         fo = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fo)));
-        if (!fmap) to_keys();
+        if (!vmap) to_keys();
     }
-    const bool vmap = F32 && fmap;
     zero_hist(hist, R0, lane);
     __builtin_amdgcn_wave_barrier();
     uint32_t *mine = hist + (lane % R0) * RW_STRIDE;
-    if (vmap) {
+    // each loop exists once per map (no per-key branch on the map)
+    if (F32 && vmap) {
 #pragma unroll
         for (int j = 0; j < KPL; ++j) atomicAdd(&mine[vbin(__uint_as_float(key[j]), fs, fo)], 1u);
     } else {
@@ -423,40 +442,107 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     wave_pick(hist, R0, lane, kk, bin, below, cnt);
     __builtin_amdgcn_wave_barrier();  // every lane's histogram reads before the list overwrites it
     if (cnt > (uint32_t)WAVE) {
-        if (vmap) to_keys();
-        return row_select_radix<KPL, R0>(key, hist, lane, kk);
+        if (F32 && vmap) to_keys();
+        const uint32_t ans = row_select_radix<KPL, R0>(key, hist, lane, kk);
+        if (eq_out) {
+            uint32_t e = 0;
+#pragma unroll
+            for (int j = 0; j < KPL; ++j) e += key[j] == ans ? 1u : 0u;
+            *eq_out = wave_reduce(e, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+        }
+        return ans;
     }
     kk -= below;
 
     // filter the bin's keys into the list (the histogram words)
-    // vbin(v) == B  <=>  B <= t < B + 1 for t = fma(v, s, o) (the clamp only
-    // merges t < 0 into bin 0 and t >= 255 into bin 255): one fma, two compares
-    const float s2 = opaque(fs), o2 = opaque(fo);  // recompute t, do not keep the bins
-    // (bin 0 takes t = -inf, bin 255 takes t = +inf: infinities clamp there and
-    // t >= NaN is false)
-    const float tlo = bin ? (float)bin : -__builtin_inff(), thi = bin < 255u ? (float)(bin + 1) : __builtin_nanf("");
-    const uint32_t lo = opaque(bin << 24);  // top-byte bin B = keys [B << 24, +2^24)
+    // The lanes holding one (the compare's mask is the execution mask of the
+    // store, so the position is mbcnt of exec: no per-key boolean in a VGPR).
     uint32_t fill = 0;
-#pragma unroll
-    for (int j = 0; j < KPL; ++j) {
-        bool in;
-        if (vmap) {
-            const float t = __builtin_fmaf(__uint_as_float(key[j]), s2, o2);
-            in = t >= tlo && !(t >= thi);
-        } else {
-            in = key[j] - lo <= 0x00FFFFFFu;
-        }
+    auto append = [&](bool in, uint32_t x) __attribute__((always_inline)) {
         const unsigned long long B = __ballot(in);
-        if (B) {  // wave-uniform
-            const uint32_t pos =
-                fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
-            if (in) hist[pos] = key[j];
-            fill += (uint32_t)__popcll(B);
+        if (in) {
+            const unsigned long long E = __builtin_amdgcn_read_exec();
+            hist[fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(E >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)E, 0u))] = x;
         }
+        fill += (uint32_t)__popcll(B);
+    };
+    const bool stage = STAGE && 2 * (below + cnt) + STAGE_OFF <= (uint32_t)(R0 * RW_STRIDE);  // wave-uniform
+    if (STAGE && stage) {
+        // per group of 4 keys a lane (columns e + q, lane-major): the four ballots
+        // of the staged keys give each lane its column-order position
+        uint2 *pairs = reinterpret_cast<uint2 *>(hist + STAGE_OFF);
+        uint32_t staged = 0;
+        uint32_t e0;
+        asm volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(e0) : "v"(lane));  // per row: not hoisted and spilled
+        const float s2 = opaque(fs);
+        float o2;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
+        const uint32_t ob = opaque(bin);
+        const uint32_t lo = opaque(bin << 24), hi_edge = lo | 0x00FFFFFFu;
+        // one loop per map (no per-key branch on it)
+        auto stage_rows = [&](auto vm) __attribute__((always_inline)) {
+            constexpr bool VM = decltype(vm)::value;
+#pragma unroll
+            for (int g = 0; g < KPL / 4; ++g) {
+                bool c[4];
+                unsigned long long bc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t x = key[4 * g + q];
+                    bool in;
+                    if constexpr (VM) {
+                        const uint32_t b = vbin(__uint_as_float(x), s2, o2);
+                        in = b == ob;
+                        c[q] = b <= ob;
+                    } else {
+                        in = x - lo <= 0x00FFFFFFu;
+                        c[q] = x <= hi_edge;
+                    }
+                    append(in, x);
+                    bc[q] = __ballot(c[q]);
+                }
+                if ((bc[0] | bc[1] | bc[2] | bc[3]) != 0) {  // wave-uniform
+                    uint32_t pos = staged;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bc[q] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bc[q], pos));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (c[q]) {
+                            const uint32_t x = key[4 * g + q];
+                            pairs[pos] = make_uint2(VM ? x : raw_of_key<F32>(x ^ flip), e0 + (uint32_t)(g * WAVE * 4 + q));
+                        }
+                        pos += c[q] ? 1u : 0u;
+                        staged += (uint32_t)__popcll(bc[q]);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+            }
+        };
+        if (F32 && vmap)
+            stage_rows(std::true_type{});
+        else
+            stage_rows(std::false_type{});
+    } else if (F32 && vmap) {
+        // the bin recomputed exactly as pass A did (fma, clamp, convert) and one
+        // compare: a single mask per key.  The offset sits in a VGPR (an fma reads
+        // at most one SGPR on gfx9); opaque copies keep pass A's per-key values
+        // from being kept live until here.
+        const float s2 = opaque(fs);
+        float o2;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
+        const uint32_t ob = opaque(bin);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) append(vbin(__uint_as_float(key[j]), s2, o2) == ob, key[j]);
+    } else {
+        const uint32_t lo = opaque(bin << 24);  // top-byte bin B = keys [B << 24, +2^24)
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) append(key[j] - lo <= 0x00FFFFFFu, key[j]);
     }
     __builtin_amdgcn_wave_barrier();
     const uint32_t L = cnt;  // == fill
-    if (vmap) {  // raw bits -> order keys, in the list
+    if (F32 && vmap) {  // raw bits -> order keys, in the list
         if ((uint32_t)lane < L) hist[lane] = key_of_f32(hist[lane]) ^ flip;
         __builtin_amdgcn_wave_barrier();
     }
@@ -471,8 +557,37 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     const int f = bm ? __ffsll((long long)bm) - 1 : 0;
     const uint32_t answer = lane_val(my, f);
     kk -= lane_val(lt, f);
+    if (eq_out) *eq_out = lane_val(le, f) - lane_val(lt, f);  // every key equal to the answer is listed
     __builtin_amdgcn_wave_barrier();
-    if (KEYS_OUT && vmap) to_keys();
+    if (STAGE && stage) {
+        // the staged pairs in column order: keep the keys below the k-th and the
+        // first kk keys equal to it (ties by column)
+        const uint2 *pairs = reinterpret_cast<const uint2 *>(hist + STAGE_OFF);
+        const uint32_t nc = below + cnt;
+        uint32_t out = 0, eq_seen = 0;
+        for (uint32_t b0 = 0; b0 < nc; b0 += WAVE) {  // wave-uniform
+            const uint32_t i = b0 + (uint32_t)lane;
+            const bool valid = i < nc;
+            const uint2 pr = valid ? pairs[i] : make_uint2(0u, 0u);
+            const uint32_t u = (F32 ? key_of_f32(pr.x) : key_of_i32(pr.x)) ^ flip;
+            const bool lt2 = valid && u < answer, eq2 = valid && u == answer;
+            const unsigned long long be = __ballot(eq2);
+            const uint32_t rank = eq_seen + __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
+            const bool keep = lt2 || (eq2 && rank < kk);
+            const unsigned long long bk = __ballot(keep);
+            const uint32_t pos = out + __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, 0u));
+            if (keep) {
+                if (tko->vals) tko->vals[tko->obase + pos] = pr.x;
+                if (tko->idx) tko->idx[tko->obase + pos] = (int32_t)pr.y;
+            }
+            out += (uint32_t)__popcll(bk);
+            eq_seen += (uint32_t)__popcll(be);
+        }
+        *topk_done = true;
+        __builtin_amdgcn_wave_barrier();
+        return answer;
+    }
+    if (KEYS_OUT && F32 && vmap) to_keys();
     return answer;
 }
 
@@ -494,13 +609,15 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
     for (u64 r = wave0; r < rows; r += nwaves) {  // wave-uniform
         const uint32_t *row = m + r * (u64)cols;
         uint32_t key[KPL];
-        uint32_t kk = k, answer;
+        uint32_t kk = k, answer, eqn = 0;  // eqn: keys equal to the answer (FULL rows; 0 = unknown)
+        bool topk_done = false;            // the fast path wrote the row's top-k itself
         if (FULL) {
 #pragma unroll
             for (int j = 0; j < KPL / 4; ++j) {
-                // top-k re-reads the row for its compaction: keep it in L2 (no non-temporal hint)
+                // (top-k rows whose bins cannot be staged re-read the row; with
+                // the non-temporal hint that re-read comes from HBM, not L2 -- rare)
                 const uint4 *src = reinterpret_cast<const uint4 *>(row + (j * WAVE + lane) * 4);
-                const uint4 x = TOPK_RELOAD && TOPK ? *src : load_nt(src);
+                const uint4 x = TOPK && !KTH_TOPK_NT ? *src : load_nt(src);
                 key[4 * j + 0] = x.x;
                 key[4 * j + 1] = x.y;
                 key[4 * j + 2] = x.z;
@@ -508,7 +625,12 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
             }
             if (!F32) {
 #pragma unroll
-                for (int j = 0; j < KPL; ++j) key[j] = key_of_i32(key[j]) ^ flip;
+                for (int j = 0; j < KPL; ++j) {
+                    key[j] = key_of_i32(key[j]) ^ flip;
+                    // opaque: later uses of the raw value recompute it from the key
+                    // instead of keeping the loaded word live beside it (VGPRs)
+                    if (TOPK) asm volatile("" : "+v"(key[j]));
+                }
             }
 #ifdef KTH_ROWS_LEGACY
             if (F32) {
@@ -517,7 +639,9 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
             }
             answer = row_select_radix<KPL, R0>(key, hist, lane, kk);
 #else
-            answer = row_select_fast<F32, KPL, R0, TOPK>(key, hist, lane, kk, TOPK ? flip : 0u);
+            const TopkOut tko{k, vals, idx, r * (u64)k};
+            answer = row_select_fast<F32, KPL, R0, TOPK, TOPK>(key, hist, lane, kk, TOPK ? flip : 0u,
+                                                                TOPK ? &eqn : nullptr, &tko, &topk_done);
 #endif
         } else {
 #pragma unroll
@@ -545,7 +669,7 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
         }
         if (!TOPK) {
             if (lane == 0) out[r] = raw_of_key<F32>(answer ^ flip);
-        } else {
+        } else if (!topk_done) {
             // Compaction in column order.  Group j holds columns (64*j + lane)*4 + q:
             // lane-major, then q.  For each q a ballot of the selected keys and
             // mbcnt (set bits in lower lanes) give every key its position: the
@@ -597,7 +721,62 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
                 taken += tot;
                 eq_seen += eq_tot;
             };
-            if (TOPK_RELOAD && FULL) {
+            // Every key equal to the k-th is kept (kk == eqn: always for rows of
+            // distinct keys): the kept keys are exactly key <= answer, one compare
+            // each.  Per group, the four ballots of the kept keys give each lane its
+            // position (mbcnt of the lanes below, plus its own earlier q); the
+            // (value, column) pairs go to LDS as one 8-byte write.
+            auto group_all = [&](uint32_t e, const uint32_t (&g)[4]) __attribute__((always_inline)) {
+                bool sel[4];
+                unsigned long long bs[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    sel[q] = g[q] <= answer;
+                    bs[q] = __ballot(sel[q]);
+                }
+                if ((bs[0] | bs[1] | bs[2] | bs[3]) == 0) return;  // wave-uniform
+                uint32_t pos = taken;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bs[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bs[q], pos));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (sel[q]) {
+                        const uint32_t x = raw_of_key<F32>(g[q] ^ flip);
+                        if (stage) {
+                            reinterpret_cast<uint2 *>(hist)[pos] = make_uint2(x, e + q);
+                        } else {
+                            if (vals) vals[obase + pos] = x;
+                            if (idx) idx[obase + pos] = (int32_t)(e + q);
+                        }
+                    }
+                    pos += sel[q] ? 1u : 0u;
+                    taken += (uint32_t)__popcll(bs[q]);
+                }
+            };
+            const bool all_ties = FULL && kk == eqn;
+            if (TOPK_RELOAD && FULL && all_ties) {
+                // the row again, from L2, every group's load in flight at once (the
+                // keys' registers are free by now): one round trip per row, not
+                // one per two groups
+                const uint4 *src = reinterpret_cast<const uint4 *>(row);
+                uint4 xr[KPL / 4];
+#pragma unroll
+                for (int j = 0; j < KPL / 4; ++j) xr[j] = src[j * WAVE + lane];
+                // columns from a per-row copy of 4 * lane: hoisted out of the row
+                // loop, the sixteen group columns were spilled to scratch
+                uint32_t e0;
+                asm volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(e0) : "v"(lane));
+#pragma unroll
+                for (int j = 0; j < KPL / 4; ++j) {
+                    const uint32_t raw[4] = {xr[j].x, xr[j].y, xr[j].z, xr[j].w};
+                    uint32_t g[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) g[q] = (F32 ? key_of_f32(raw[q]) : key_of_i32(raw[q])) ^ flip;
+                    group_all(e0 + (uint32_t)(j * WAVE * 4), g);
+                    __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+                }
+            } else if (TOPK_RELOAD && FULL) {
                 // FULL rows re-read their keys here (from L2: loaded without the
                 // non-temporal hint), two groups ahead, in a rolled loop, instead of
                 // keeping all KPL keys live through the compaction: 4 waves per
