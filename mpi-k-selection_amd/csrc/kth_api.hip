@@ -45,6 +45,18 @@ int gather_grid(u64 nchunks) {
     return (int)std::max<u64>(1, (nchunks + per_wg - 1) / per_wg);
 }
 constexpr size_t ISLOT_WORDS = 3 * (size_t)kth::STATS_WORDS + 2;  // 3 slots + cand_count + pad
+// after the islots, in the same allocation: k_head's and k_finish's level
+// slots (zero between selects), then the grid-barrier words (never cleared by
+// a select: the barrier resets itself)
+constexpr size_t HSLOT_OFF = ISLOT_WORDS;
+constexpr size_t HSLOT_WORDS = (size_t)kth::HEAD_LEVELS * kth::STATS_WORDS;
+constexpr size_t FSLOT_OFF = HSLOT_OFF + HSLOT_WORDS;  // two sets, alternate k_finish launches
+constexpr size_t FSLOT_WORDS = (size_t)kth::FIN_LEVELS * kth::STATS_WORDS;
+constexpr size_t ZERO_WORDS = FSLOT_OFF + 2 * FSLOT_WORDS;
+constexpr size_t BAR_OFF = ZERO_WORDS;
+constexpr size_t SLOT_ALLOC_WORDS = BAR_OFF + kth::BAR_WORDS / 2;
+constexpr u64 FIN_SPARSE_PER_WG = (u64)kth::DENSE_BLK * kth::FIN_UNROLL * 4;  // one k_finish tile
+constexpr double HEAD_SLACK = 1.5;  // k_head early window (EarlyWindow); KTH_HEAD_SLACK overrides, 0 = off
 static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
 
@@ -72,6 +84,10 @@ struct kth_ctx {
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
+    bool coop = true;          // window / radix paths as k_head + k_main + k_finish (KTH_COOP=0: per-level launches)
+    int fin_grid = 256;        // k_finish workgroups (one per CU; KTH_FIN_GRID)
+    uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
+    int fin_set = 0;           // k_finish slot set of the next launch (the other one is cleared by it)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -303,7 +319,46 @@ int run_small(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
     return launch_check();
 }
 
+kth::CoopArgs coop_args(kth_ctx *c, u64 slot_off, int32_t *d_out, int32_t *d_status) {
+    kth::CoopArgs x;
+    memset(&x, 0, sizeof x);
+    x.slots = c->islots + slot_off;
+    x.bar = reinterpret_cast<uint32_t *>(c->islots + BAR_OFF);
+    x.d_out = d_out;
+    x.d_status = d_status;
+    x.dense_per_wg = DENSE_PER_WG;
+    x.sparse_per_wg = FIN_SPARSE_PER_WG;
+    x.slack64 = c->head_slack64;
+    return x;
+}
+
+// k_finish: the finish phase in one launch, on slot set fin_set; it clears the
+// other set and the sample phase's slots for the next select
+constexpr size_t FIN_DYN_LDS = (size_t)kth::FIN_LDS_KEYS * 4;
+void launch_finish(kth_ctx *c, StepArgs a, int32_t *d_out, int32_t *d_status) {
+    const size_t mine = FSLOT_OFF + (size_t)c->fin_set * FSLOT_WORDS;
+    a.stats_zero = c->islots + FSLOT_OFF + (size_t)(1 - c->fin_set) * FSLOT_WORDS;
+    a.zero_words = FSLOT_WORDS;
+    kth::CoopArgs x = coop_args(c, mine, d_out, d_status);
+    x.zero2 = c->islots + HSLOT_OFF;
+    x.zero2_words = HSLOT_WORDS;
+    kth::k_finish<<<c->fin_grid, kth::DENSE_BLK, FIN_DYN_LDS, c->stream>>>(a, x);
+    c->fin_set ^= 1;
+}
+
 int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status) {
+    if (c->coop) {  // three radix levels over the input in one launch
+        StepArgs a = step(c, kth::ADV_INIT_FULL, -1, 1, nullptr, nullptr, nullptr);
+        a.keys = keys;
+        a.n_local = (u64)n;
+        a.init_n = (u64)n;
+        a.init_k = (u64)k;
+        ev_main(c);
+        launch_finish(c, a, d_out, d_status);
+        ev_main(c);
+        c->last_state = 1;
+        return launch_check();
+    }
     StepArgs a = step(c, kth::ADV_INIT_FULL, -1, 0, nullptr, islot(c, 1), islot(c, 2));
     a.keys = keys;
     a.n_local = (u64)n;
@@ -339,6 +394,38 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     KTH_TRY(grow(reinterpret_cast<void **>(&c->sample), &c->sample_cap, (u64)s * 4));
     KTH_TRY(reserve_cand(c, n));
 
+    if (c->coop) {
+        // sample phase in one launch -> window state in st[0]
+        // (it also clears the streaming pass's count slot islot(1) and the candidate count)
+        StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, nullptr, islot(c, 1));
+        a.zero_words = 2 * (u64)kth::STATS_WORDS + 1;
+        a.init_n = (u64)n;
+        a.init_k = (u64)k;
+        a.init_s = (u64)s;
+        a.r_lo = r_lo;
+        a.r_hi = r_hi;
+        kth::k_head<<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, coop_args(c, HSLOT_OFF, nullptr, nullptr),
+                                                                          keys, (u64)n, stride, c->sample, (u64)s);
+        // the streaming pass: counts into islot(1) (zero between selects)
+        a = step(c, kth::ADV_CARRY, 0, 1, nullptr, islot(c, 1), nullptr);
+        a.keys = keys;
+        a.n_local = (u64)n;
+        ev_main(c);
+        if (tflag == 1)
+            kth::k_main<1><<<c->main_grid[1], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+        else if (tflag == 2)
+            kth::k_main<2><<<c->main_grid[2], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
+        else
+            kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+        ev_main(c);
+        // decide + candidate (or fallback) levels + answer in one launch
+        a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), nullptr, nullptr);
+        a.keys = keys;
+        a.n_local = (u64)n;
+        launch_finish(c, a, d_out, d_status);
+        c->last_state = 0;
+        return launch_check();
+    }
     // sample + first digit of the sample
     StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
     a.init_n = (u64)n;
@@ -395,7 +482,7 @@ int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_
     if (!c || !d_keys || (!d_out && !d_status) || n < 1 || k < 1 || k > n) return KTH_EINVAL;
     KTH_TRY(set_device(c));
     if (c->dirty) {
-        HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
+        HIP_TRY(hipMemsetAsync(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64), c->stream));
         c->dirty = false;
     }
     int rc;
@@ -450,7 +537,9 @@ int launch_rows(kth_ctx *c, const uint32_t *d_keys, int64_t rows, int32_t cols, 
                 uint32_t flip = 0, uint32_t *vals = nullptr, int32_t *idx = nullptr) {
     const bool vec = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0 && cols % 4 == 0;
     const int rows_per_wg = kth::RW_BLOCK / kth::WAVE;
-    const int g = (int)std::min<int64_t>((rows + rows_per_wg - 1) / rows_per_wg, (int64_t)c->num_cu * 64);
+    const int64_t g64 = (rows + rows_per_wg - 1) / rows_per_wg;  // one row per wave
+    if (g64 > 0x7FFFFFFF) return KTH_EINVAL;
+    const int g = (int)g64;
     const u64 R = (u64)rows;
     const uint32_t C = (uint32_t)cols, K = (uint32_t)k;
     if (cols <= 1024)
@@ -543,6 +632,10 @@ int kth_ctx_create(int device, kth_ctx **out) {
             if (const char *g = getenv("KTH_SPARSE_PER_WG")) c->sparse_per_wg = (u64)std::max(0, atoi(g));
             if (const char *g = getenv("KTH_POST_DENSE_GRID")) c->post_dense_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
+            if (const char *g = getenv("KTH_COOP")) c->coop = atoi(g) != 0;
+            c->fin_grid = c->num_cu;
+            if (const char *g = getenv("KTH_FIN_GRID")) c->fin_grid = std::max(1, std::min(atoi(g), c->num_cu));
+            if (const char *g = getenv("KTH_HEAD_SLACK")) c->head_slack64 = (uint32_t)std::max(0.0, atof(g) * 64.0);
             // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
             // so its count pass must report the bracket failure
             c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
@@ -550,7 +643,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
         if (hipMalloc(reinterpret_cast<void **>(&c->st), 2 * sizeof(SelState)) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void **>(&c->islots), ISLOT_WORDS * sizeof(u64)) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void **>(&c->islots), SLOT_ALLOC_WORDS * sizeof(u64)) != hipSuccess ||
             hipMalloc(reinterpret_cast<void **>(&c->d_status), 4 * sizeof(int32_t)) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void **>(&c->h_status), 4 * sizeof(int32_t), 0) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void **>(&c->h_state), sizeof(SelState), 0) != hipSuccess) {
@@ -558,7 +651,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             break;
         }
         if (hipMemset(c->st, 0, 2 * sizeof(SelState)) != hipSuccess ||
-            hipMemset(c->islots, 0, ISLOT_WORDS * sizeof(u64)) != hipSuccess) {
+            hipMemset(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64)) != hipSuccess) {
             rc = KTH_EHIP;
             break;
         }
@@ -569,6 +662,9 @@ int kth_ctx_create(int device, kth_ctx **out) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, KTH_ROWS_MAX_COLS * 4);
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kth::k_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, KTH_ROWS_MAX_COLS * 4);
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(kth::k_finish),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)FIN_DYN_LDS) != hipSuccess)
+            c->coop = false;  // no LDS-resident finish: per-level launches
         (void)hipGetLastError();
     } while (0);
     if (rc != KTH_OK) {
@@ -856,7 +952,7 @@ int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     c->dist_zero = true;  // kth_dist_sample clears the slots inside its kernel
     // the ctx's own slots are left zeroed by every completed k_result; a
     // sequence cut short (dirty, or a dist selection never finished) re-zeroes
-    if (c->dirty || c->dist_open) HIP_TRY(hipMemsetAsync(c->islots, 0, ISLOT_WORDS * sizeof(u64), c->stream));
+    if (c->dirty || c->dist_open) HIP_TRY(hipMemsetAsync(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64), c->stream));
     c->dirty = false;
     c->dist_open = true;
     return KTH_OK;

@@ -41,6 +41,7 @@ enum : int {
     ADV_INIT_FULL = 1,    // fresh selection, plain radix passes over the input
     ADV_PICK = 2,         // consume the previous digit's reduced histogram
     ADV_DECIDE = 3,       // consume the streaming pass's reduced counts
+    ADV_CARRY = 4,        // take the previous kernel's state as is (it resolved its own digits)
 };
 
 struct Target {
@@ -58,7 +59,9 @@ struct alignas(16) SelState {
     Target t[2];
     uint32_t mode, W, base, lo, hi, answer, error, path;
     uint32_t share;    // target 1 reads target 0's histogram this level
-    uint32_t pad[3];
+    uint32_t d0;       // width of a domain's first digit (0: DIGIT); later digits are DIGIT wide
+    uint32_t pad[2];
+    u64 below, eqv;    // done: keys below the answer, keys equal to it (0 = unknown); kth_topk_i32
 };
 
 __device__ __forceinline__ uint32_t key_of_i32(uint32_t bits) { return bits ^ 0x80000000u; }
@@ -77,6 +80,11 @@ __device__ __forceinline__ uint32_t f32_of_key(uint32_t key) {
 __device__ __forceinline__ uint32_t digit_bits(uint32_t W, uint32_t done) {
     uint32_t r = W - done;
     return r < (uint32_t)DIGIT ? r : (uint32_t)DIGIT;
+}
+// the next digit of a selection state: the first one may be narrower (d0)
+__device__ __forceinline__ uint32_t digit_bits(const SelState &s, uint32_t done) {
+    const uint32_t r = s.W - done, d = (done == 0 && s.d0) ? s.d0 : (uint32_t)DIGIT;
+    return r < d ? r : d;
 }
 
 // does v (= key - base) match target's resolved prefix?
@@ -211,10 +219,11 @@ __device__ __forceinline__ u64 wave_incl_scan64(u64 x) {
 // thread i owning bins [i*PER, i*PER + PER)): one wave scan per target, both
 // chains interleaved, and two barriers in all.  want[t] = false skips target
 // t (its outputs are then unspecified).  ok[t] false if the histogram holds
-// fewer than k[t] keys.  `scratch` holds 2 * (BLOCK/64) + 6 words.
+// fewer than k[t] keys; cnt[t] = keys in the picked bin.  `scratch` holds
+// 2 * (BLOCK/64) + 8 words.
 template <int BLOCK, int PER>
 __device__ void block_pick2(const u64 (&h0)[PER], const u64 (&h1)[PER], const bool want[2], const u64 k[2],
-                            uint32_t bin[2], u64 below[2], bool ok[2], u64 *scratch) {
+                            uint32_t bin[2], u64 below[2], bool ok[2], u64 *scratch, u64 cnt[2]) {
     constexpr int NW = BLOCK / WAVE;
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     u64 sum0 = 0, sum1 = 0;
@@ -229,7 +238,7 @@ __device__ void block_pick2(const u64 (&h0)[PER], const u64 (&h1)[PER], const bo
         wsum[wid] = inc0;
         wsum[NW + wid] = inc1;
     }
-    if (threadIdx.x < 6) res[threadIdx.x] = 0;
+    if (threadIdx.x < 8) res[threadIdx.x] = 0;
     __syncthreads();
     u64 pre0 = inc0 - sum0, pre1 = inc1 - sum1;
 #pragma unroll
@@ -249,9 +258,10 @@ __device__ void block_pick2(const u64 (&h0)[PER], const u64 (&h1)[PER], const bo
             for (int j = 0; j < PER; ++j) {
                 const u64 hj = t ? h1[j] : h0[j];
                 if (!found && cum + hj >= kt) {
-                    res[3 * t + 0] = 1;
-                    res[3 * t + 1] = (u64)(threadIdx.x * PER + j);
-                    res[3 * t + 2] = cum;
+                    res[4 * t + 0] = 1;
+                    res[4 * t + 1] = (u64)(threadIdx.x * PER + j);
+                    res[4 * t + 2] = cum;
+                    res[4 * t + 3] = hj;
                     found = true;
                 }
                 cum += hj;
@@ -261,9 +271,10 @@ __device__ void block_pick2(const u64 (&h0)[PER], const u64 (&h1)[PER], const bo
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-        ok[t] = res[3 * t] != 0;
-        bin[t] = (uint32_t)res[3 * t + 1];
-        below[t] = res[3 * t + 2];
+        ok[t] = res[4 * t] != 0;
+        bin[t] = (uint32_t)res[4 * t + 1];
+        below[t] = res[4 * t + 2];
+        cnt[t] = res[4 * t + 3];
     }
 }
 

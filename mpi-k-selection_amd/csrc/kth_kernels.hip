@@ -140,6 +140,71 @@ __device__ __forceinline__ void decide(SelState &s, const u64 *c) {
     }
 }
 
+// Early window (cooperative head only): once both window targets have picked
+// a digit, the window may stop at the current digit resolution -- lo = lower
+// edge of r_lo's bin, hi = upper edge of r_hi's bin -- when the sample keys
+// inside those edges are within `slack64`/64 of the r_hi - r_lo + 1 the exact
+// window holds.  Any [lo, hi] keeps decide() exact; this only trades a wider
+// window (more candidates) for fewer sample levels.  A heavy-duplicate bin
+// fails the test and keeps refining, down to exact sample keys.
+struct EarlyWindow {
+    u64 r_lo, r_hi;   // the sample ranks of the targets (0 / s+1: no bound)
+    uint32_t slack64; // 0: off
+};
+
+__device__ __forceinline__ void early_window(SelState &s, const EarlyWindow &e, u64 cnt1) {
+    if (e.slack64 == 0 || s.mode != MODE_SAMPLE) return;
+    const bool a0 = s.t[0].active, a1 = s.t[1].active;
+    if ((a0 && s.t[0].done == 0) || (a1 && s.t[1].done == 0)) return;
+    const u64 below0 = a0 ? e.r_lo - s.t[0].k : 0;           // sample keys under r_lo's bin
+    const u64 upto1 = a1 ? e.r_hi - s.t[1].k + cnt1 : s.s;    // sample keys up to r_hi's bin's top
+    const u64 want = (a1 ? e.r_hi : s.s) - (a0 ? e.r_lo : 1) + 1;
+    if (upto1 < below0 || (upto1 - below0) * 64 > want * (u64)e.slack64) return;
+    const uint32_t w0 = s.W - s.t[0].done, w1 = s.W - s.t[1].done;
+    s.lo = a0 ? s.base + (w0 >= 32 ? 0u : s.t[0].prefix << w0) : 0u;
+    s.hi = a1 ? s.base + (w1 >= 32 ? 0xFFFFFFFFu : (s.t[1].prefix << w1) | ((1u << w1) - 1u)) : 0xFFFFFFFFu;
+    s.mode = MODE_MAIN;
+}
+
+// Pick every live target's next digit from a histogram the caller holds in
+// registers (thread i owns bins [i*PER, i*PER + PER) of target t in h[t];
+// `share`: target 1 reads target 0's histogram).  Thread 0 updates ss; ends
+// with a barrier.
+template <int BLOCK, int PER>
+__device__ __forceinline__ void pick_state(SelState &ss, const u64 (&h0)[PER], const u64 (&h1)[PER], bool share,
+                                           u64 *scratch, const EarlyWindow *ew = nullptr) {
+    const uint32_t mode = ss.mode;
+    const bool live = mode == MODE_SAMPLE || mode == MODE_CAND || mode == MODE_FULL;
+    bool want[2];
+    u64 kt[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        want[t] = live && ss.t[t].active && ss.t[t].done < ss.W;
+        kt[t] = ss.t[t].k;
+    }
+    uint32_t bin[2];
+    u64 below[2], cnt[2] = {0, 0};
+    bool ok[2];
+    if (want[0] || want[1]) block_pick2<BLOCK, PER>(h0, share ? h0 : h1, want, kt, bin, below, ok, scratch, cnt);
+    if (threadIdx.x == 0) {
+        for (int t = 0; t < 2; ++t) {
+            if (!want[t] || ss.mode == MODE_DONE) continue;
+            const uint32_t d = digit_bits(ss, ss.t[t].done);
+            if (!ok[t] || bin[t] >= (1u << d)) {
+                ss.error = 1 + t;
+                ss.mode = MODE_DONE;
+            } else {
+                ss.t[t].k -= below[t];
+                ss.t[t].prefix = (ss.t[t].prefix << d) | bin[t];
+                ss.t[t].done += d;
+            }
+        }
+        resolve(ss);
+        if (ew && want[0] == ss.t[0].active && want[1] == ss.t[1].active) early_window(ss, *ew, cnt[1]);
+    }
+    __syncthreads();
+}
+
 template <int BLOCK>
 __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
     // Histogram words are loaded by every thread up front, in parallel with the
@@ -154,6 +219,11 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
     const bool carry = a.adv != ADV_INIT_SAMPLE && a.adv != ADV_INIT_FULL;
     uint4 sv = make_uint4(0u, 0u, 0u, 0u);
     if (carry && threadIdx.x < SV) sv = reinterpret_cast<const uint4 *>(a.st_in)[threadIdx.x];
+    // the streaming pass's counts travel with the state (one round trip)
+    constexpr int CT = (SV + WAVE - 1) / WAVE * WAVE;  // first thread of the counts (next wave)
+    static_assert(CT + NCOUNTS <= BLOCK, "counts load beside the state");
+    u64 cv = 0;
+    if (a.adv == ADV_DECIDE && threadIdx.x >= CT && threadIdx.x < CT + NCOUNTS) cv = a.stats_in[threadIdx.x - CT];
     u64 h0[PER], h1[PER];
     if (a.adv == ADV_PICK) {
         const u64 *b0 = a.stats_in + NCOUNTS + threadIdx.x * PER;
@@ -189,43 +259,15 @@ __device__ void advance(SelState &ss, const StepArgs &a, u64 *scratch) {
         }
     }
     if (carry && threadIdx.x < SV) reinterpret_cast<uint4 *>(&ss)[threadIdx.x] = sv;
+    if (a.adv == ADV_DECIDE && threadIdx.x >= CT && threadIdx.x < CT + NCOUNTS) scratch[threadIdx.x - CT] = cv;
     __syncthreads();
     if (a.adv == ADV_DECIDE) {
-        if (threadIdx.x == 0 && ss.mode == MODE_MAIN) decide(ss, a.stats_in);
+        if (threadIdx.x == 0 && ss.mode == MODE_MAIN) decide(ss, scratch);
         __syncthreads();
     } else if (a.adv == ADV_PICK) {
         // both targets' digits in one pass (two barriers); target 1 reads
         // target 0's histogram when they share a prefix
-        const uint32_t mode = ss.mode;
-        const bool live = mode == MODE_SAMPLE || mode == MODE_CAND || mode == MODE_FULL;
-        bool want[2];
-        u64 kt[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            want[t] = live && ss.t[t].active && ss.t[t].done < ss.W;
-            kt[t] = ss.t[t].k;
-        }
-        const bool share = ss.share;
-        uint32_t bin[2];
-        u64 below[2];
-        bool ok[2];
-        if (want[0] || want[1]) block_pick2<BLOCK, PER>(h0, share ? h0 : h1, want, kt, bin, below, ok, scratch);
-        if (threadIdx.x == 0) {
-            for (int t = 0; t < 2; ++t) {
-                if (!want[t] || ss.mode == MODE_DONE) continue;
-                const uint32_t d = digit_bits(ss.W, ss.t[t].done);
-                if (!ok[t] || bin[t] >= (1u << d)) {
-                    ss.error = 1 + t;
-                    ss.mode = MODE_DONE;
-                } else {
-                    ss.t[t].k -= below[t];
-                    ss.t[t].prefix = (ss.t[t].prefix << d) | bin[t];
-                    ss.t[t].done += d;
-                }
-            }
-            resolve(ss);
-        }
-        __syncthreads();
+        pick_state<BLOCK, PER>(ss, h0, h1, ss.share, scratch);
     }
 }
 
@@ -305,7 +347,7 @@ __device__ __forceinline__ HistPlan make_plan(const SelState &ss, bool *share) {
     p.base = ss.base;
     for (int t = 0; t < 2; ++t) {
         p.h[t] = live && ss.t[t].active && ss.t[t].done < ss.W;
-        const uint32_t d = p.h[t] ? digit_bits(ss.W, ss.t[t].done) : 0u;
+        const uint32_t d = p.h[t] ? digit_bits(ss, ss.t[t].done) : 0u;
         p.done[t] = ss.t[t].done;
         p.prefix[t] = ss.t[t].prefix;
         p.shift[t] = p.h[t] ? ss.W - ss.t[t].done - d : 0u;
@@ -397,34 +439,20 @@ __global__ __launch_bounds__(BLOCK) void k_level(StepArgs a) {
     KTH_STAMP(a, 5);
 }
 
-// Sample gather: s keys in chunks of 64 contiguous keys spread evenly over the
-// shard (stride = chunk distance in keys).  With FUSE the first digit's
-// histogram of the sample is built too (single-GPU: the sample is complete).
-template <bool FUSE>
-__global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 n_keys,
-                                                u64 stride, uint32_t *__restrict__ sample, u64 s) {
-    __shared__ SelState ss;
-    __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
-    __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
-    HistPlan plan;
-    bool share = false;
-    KTH_STAMP(a, 0);
-    if (FUSE) {
-        advance<DENSE_BLK>(ss, a, scratch);
-        plan = make_plan(ss, &share);
-        publish<DENSE_BLK>(ss, share, a);
-        for (int i = threadIdx.x; i < 2 * NBINS; i += DENSE_BLK) (&lh[0][0])[i] = 0;
-        __syncthreads();
-    }
-    if (!FUSE) {  // the sharded protocol's slots, cleared here instead of by a memset launch
-        for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < a.zero_words; i += (u64)gridDim.x * DENSE_BLK)
-            a.stats_zero[i] = 0;
-    }
+// Sample gather: s keys in chunks of SAMPLE_CHUNK contiguous keys spread
+// evenly over the shard (stride = chunk distance in keys), by waves gw of nw
+// (WAVES per workgroup).  With FUSE the keys also go into the LDS histograms
+// of `plan` (single GPU: the sample is complete).  COHERENT: write-through
+// (sc1) stores, for readers in other workgroups of the same kernel (k_head).
+template <int BLOCK, bool FUSE, bool COHERENT = false>
+__device__ __forceinline__ void gather_chunks(const int32_t *__restrict__ keys, u64 n_keys, u64 stride,
+                                              uint32_t *__restrict__ sample, u64 s, uint32_t (*lh)[NBINS],
+                                              const HistPlan &plan) {
     const int lane = threadIdx.x & (WAVE - 1);
     // chunks of SAMPLE_CHUNK keys at `stride`; the last one holds s % SAMPLE_CHUNK
     // keys when that is nonzero (scalar loads, guarded by s and n_keys)
     const u64 nfull = s / SAMPLE_CHUNK, nchunks = (s + SAMPLE_CHUNK - 1) / SAMPLE_CHUNK;
-    const u64 gw = ((u64)blockIdx.x * DENSE_BLK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (DENSE_BLK / WAVE);
+    const u64 gw = ((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (BLOCK / WAVE);
     // every wave owns GATHER_BATCH consecutive chunk slots per round; all loads
     // of a round are in flight together.  Chunks of >= 256 keys are read as
     // 16-byte loads, q-th load of the wave = 1 KiB contiguous (lane-major).
@@ -465,13 +493,40 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
                 for (int q = 0; q < SAMPLE_CK; ++q) {
                     const u64 off = off_of(q);
                     if (c * SAMPLE_CHUNK + off < s) {
-                        sample[c * SAMPLE_CHUNK + off] = kk[j][q];
-                        if (FUSE) hist_add<DENSE_BLK>(lh, plan, kk[j][q], true);
+                        if (COHERENT)
+                            __hip_atomic_store(&sample[c * SAMPLE_CHUNK + off], kk[j][q], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            sample[c * SAMPLE_CHUNK + off] = kk[j][q];
+                        if (FUSE) hist_add<BLOCK>(lh, plan, kk[j][q], true);
                     }
                 }
             }
         }
     }
+}
+
+template <bool FUSE>
+__global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t *__restrict__ keys, u64 n_keys,
+                                                u64 stride, uint32_t *__restrict__ sample, u64 s) {
+    __shared__ SelState ss;
+    __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
+    HistPlan plan{};
+    bool share = false;
+    KTH_STAMP(a, 0);
+    if (FUSE) {
+        advance<DENSE_BLK>(ss, a, scratch);
+        plan = make_plan(ss, &share);
+        publish<DENSE_BLK>(ss, share, a);
+        for (int i = threadIdx.x; i < 2 * NBINS; i += DENSE_BLK) (&lh[0][0])[i] = 0;
+        __syncthreads();
+    }
+    if (!FUSE) {  // the sharded protocol's slots, cleared here instead of by a memset launch
+        for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < a.zero_words; i += (u64)gridDim.x * DENSE_BLK)
+            a.stats_zero[i] = 0;
+    }
+    gather_chunks<DENSE_BLK, FUSE>(keys, n_keys, stride, sample, s, lh, plan);
     KTH_STAMP(a, 3);
     if (FUSE) hist_flush<DENSE_BLK>(lh, plan, a.stats_acc);
     KTH_STAMP(a, 5);
@@ -875,4 +930,5 @@ __global__ __launch_bounds__(BLK) void k_fill(int32_t *__restrict__ out, u64 n, 
 
 }  // namespace kth
 
+#include "kth_coop.hpp"
 #include "kth_rows.hpp"

@@ -378,7 +378,9 @@ struct TopkOut {
     int32_t *idx;
     u64 obase;
 };
-constexpr int STAGE_OFF = WAVE;  // staged pairs start after the list's 64 words
+constexpr int STAGE_OFF = WAVE;  // staged keys start after the list's 64 words, their columns STAGE_CAP later
+template <int R0>
+constexpr uint32_t stage_cap() { return (uint32_t)(R0 * RW_STRIDE - STAGE_OFF) / 2; }
 
 template <bool F32, int KPL, int R0, bool KEYS_OUT, bool STAGE = false>
 __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
@@ -466,11 +468,18 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
         }
         fill += (uint32_t)__popcll(B);
     };
-    const bool stage = STAGE && 2 * (below + cnt) + STAGE_OFF <= (uint32_t)(R0 * RW_STRIDE);  // wave-uniform
+    const bool stage = STAGE && below + cnt <= stage_cap<R0>();  // wave-uniform
     if (STAGE && stage) {
-        // per group of 4 keys a lane (columns e + q, lane-major): the four ballots
-        // of the staged keys give each lane its column-order position
-        uint2 *pairs = reinterpret_cast<uint2 *>(hist + STAGE_OFF);
+        // One pass stages every key of the bins up to B -- the kept keys and the
+        // rest of bin B -- as (key, column) pairs in column order: per group of
+        // 4 keys a lane (columns e + q, lane-major), the four ballots give each
+        // lane its position.  Order keys are staged as they are (value-linear
+        // rows: raw bits); the rank step's list is then read back from the
+        // staged pairs (no second compare and append per key).
+        // keys and columns in two arrays: adjacent 4-byte stores would merge into
+        // one 8-byte store, which pairs every key with a neighbour register and
+        // doubles the keys' VGPRs (spills)
+        uint32_t *skey = hist + STAGE_OFF, *scol = skey + stage_cap<R0>();
         uint32_t staged = 0;
         uint32_t e0;
         asm volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(e0) : "v"(lane));  // per row: not hoisted and spilled
@@ -478,7 +487,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
         float o2;
         asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
         const uint32_t ob = opaque(bin);
-        const uint32_t lo = opaque(bin << 24), hi_edge = lo | 0x00FFFFFFu;
+        const uint32_t hi_edge = opaque(bin << 24) | 0x00FFFFFFu;
         // one loop per map (no per-key branch on it)
         auto stage_rows = [&](auto vm) __attribute__((always_inline)) {
             constexpr bool VM = decltype(vm)::value;
@@ -489,16 +498,10 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t x = key[4 * g + q];
-                    bool in;
-                    if constexpr (VM) {
-                        const uint32_t b = vbin(__uint_as_float(x), s2, o2);
-                        in = b == ob;
-                        c[q] = b <= ob;
-                    } else {
-                        in = x - lo <= 0x00FFFFFFu;
+                    if constexpr (VM)
+                        c[q] = vbin(__uint_as_float(x), s2, o2) <= ob;
+                    else
                         c[q] = x <= hi_edge;
-                    }
-                    append(in, x);
                     bc[q] = __ballot(c[q]);
                 }
                 if ((bc[0] | bc[1] | bc[2] | bc[3]) != 0) {  // wave-uniform
@@ -507,11 +510,12 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
                     for (int q = 0; q < 4; ++q)
                         pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bc[q] >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bc[q], pos));
+                    const uint32_t colg = e0 + (uint32_t)(g * WAVE * 4);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if (c[q]) {
-                            const uint32_t x = key[4 * g + q];
-                            pairs[pos] = make_uint2(VM ? x : raw_of_key<F32>(x ^ flip), e0 + (uint32_t)(g * WAVE * 4 + q));
+                            skey[pos] = key[4 * g + q];
+                            scol[pos] = colg + (uint32_t)q;
                         }
                         pos += c[q] ? 1u : 0u;
                         staged += (uint32_t)__popcll(bc[q]);
@@ -524,6 +528,14 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             stage_rows(std::true_type{});
         else
             stage_rows(std::false_type{});
+        __builtin_amdgcn_wave_barrier();
+        // the list: the staged keys of bin B (a handful of rounds over <= nc pairs)
+        for (uint32_t i0 = 0; i0 < staged; i0 += WAVE) {  // wave-uniform
+            const uint32_t i = i0 + (uint32_t)lane;
+            const uint32_t x = i < staged ? skey[i] : 0u;
+            const bool inb = i < staged && ((F32 && vmap) ? vbin(__uint_as_float(x), s2, o2) == ob : (x >> 24) == ob);
+            append(inb, x);
+        }
     } else if (F32 && vmap) {
         // the bin recomputed exactly as pass A did (fma, clamp, convert) and one
         // compare: a single mask per key.  The offset sits in a VGPR (an fma reads
@@ -562,14 +574,14 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     if (STAGE && stage) {
         // the staged pairs in column order: keep the keys below the k-th and the
         // first kk keys equal to it (ties by column)
-        const uint2 *pairs = reinterpret_cast<const uint2 *>(hist + STAGE_OFF);
+        const uint32_t *skey = hist + STAGE_OFF, *scol = skey + stage_cap<R0>();
         const uint32_t nc = below + cnt;
         uint32_t out = 0, eq_seen = 0;
         for (uint32_t b0 = 0; b0 < nc; b0 += WAVE) {  // wave-uniform
             const uint32_t i = b0 + (uint32_t)lane;
             const bool valid = i < nc;
-            const uint2 pr = valid ? pairs[i] : make_uint2(0u, 0u);
-            const uint32_t u = (F32 ? key_of_f32(pr.x) : key_of_i32(pr.x)) ^ flip;
+            const uint2 pr = valid ? make_uint2(skey[i], scol[i]) : make_uint2(0u, 0u);
+            const uint32_t u = (F32 && vmap) ? key_of_f32(pr.x) ^ flip : pr.x;
             const bool lt2 = valid && u < answer, eq2 = valid && u == answer;
             const unsigned long long be = __ballot(eq2);
             const uint32_t rank = eq_seen + __builtin_amdgcn_mbcnt_hi((uint32_t)(be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)be, 0u));
@@ -577,7 +589,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             const unsigned long long bk = __ballot(keep);
             const uint32_t pos = out + __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, 0u));
             if (keep) {
-                if (tko->vals) tko->vals[tko->obase + pos] = pr.x;
+                if (tko->vals) tko->vals[tko->obase + pos] = (F32 && vmap) ? pr.x : raw_of_key<F32>(pr.x ^ flip);
                 if (tko->idx) tko->idx[tko->obase + pos] = (int32_t)pr.y;
             }
             out += (uint32_t)__popcll(bk);
@@ -605,8 +617,11 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
     __shared__ __attribute__((aligned(16))) uint32_t hist_all[RW_BLOCK / WAVE][R0 * RW_STRIDE];
     const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
     uint32_t *hist = hist_all[wid];
-    const u64 wave0 = (u64)blockIdx.x * (RW_BLOCK / WAVE) + wid, nwaves = (u64)gridDim.x * (RW_BLOCK / WAVE);
-    for (u64 r = wave0; r < rows; r += nwaves) {  // wave-uniform
+    // One row per wave (the grid covers the rows): a row loop let the compiler
+    // hoist per-row address arithmetic out of it and spill it (the top-k
+    // variants sit at the 128-VGPR budget of 4 waves per SIMD).
+    const u64 r = (u64)blockIdx.x * (RW_BLOCK / WAVE) + wid;
+    if (r < rows) {  // wave-uniform
         const uint32_t *row = m + r * (u64)cols;
         uint32_t key[KPL];
         uint32_t kk = k, answer, eqn = 0;  // eqn: keys equal to the answer (FULL rows; 0 = unknown)

@@ -13,7 +13,7 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
     if "kth::" in k:
         print(f"{k:40s} calls {len(v):4d} avg {sum(v) / len(v):9.1f} us  min {min(v):9.1f}")
 ks = [r for r in rows if "kth::" in r["Kernel_Name"]]
-starts = [i for i, r in enumerate(ks) if "k_gather" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(ks) if "k_gather" in r["Kernel_Name"] or "k_head" in r["Kernel_Name"]]
 if starts:
     seq = ks[starts[-1]:starts[-1] + 8]
     t0 = int(seq[0]["Start_Timestamp"])
