@@ -54,7 +54,9 @@ constexpr size_t FSLOT_OFF = HSLOT_OFF + HSLOT_WORDS;  // two sets, alternate k_
 constexpr size_t FSLOT_WORDS = (size_t)kth::FIN_LEVELS * kth::STATS_WORDS;
 constexpr size_t ZERO_WORDS = FSLOT_OFF + 2 * FSLOT_WORDS;
 constexpr size_t BAR_OFF = ZERO_WORDS;
-constexpr size_t SLOT_ALLOC_WORDS = BAR_OFF + kth::BAR_WORDS / 2;
+constexpr size_t TAIL_OFF = BAR_OFF + kth::BAR_WORDS / 2;  // k_finish's tail keys (FIN_LDS_KEYS u32)
+constexpr size_t SLOT_ALLOC_WORDS = TAIL_OFF + kth::FIN_LDS_KEYS / 2;
+static_assert(kth::BAR_TAIL % 2 == 0, "the tail word is a u64");
 constexpr u64 FIN_SPARSE_PER_WG = (u64)kth::DENSE_BLK * kth::FIN_UNROLL * 4;  // one k_finish tile
 constexpr double HEAD_SLACK = 1.5;  // k_head early window (EarlyWindow); KTH_HEAD_SLACK overrides, 0 = off
 static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
@@ -324,6 +326,7 @@ kth::CoopArgs coop_args(kth_ctx *c, u64 slot_off, int32_t *d_out, int32_t *d_sta
     memset(&x, 0, sizeof x);
     x.slots = c->islots + slot_off;
     x.bar = reinterpret_cast<uint32_t *>(c->islots + BAR_OFF);
+    x.tail = reinterpret_cast<uint32_t *>(c->islots + TAIL_OFF);
     x.d_out = d_out;
     x.d_status = d_status;
     x.dense_per_wg = DENSE_PER_WG;

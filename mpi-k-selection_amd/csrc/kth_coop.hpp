@@ -28,7 +28,8 @@ constexpr int FIN_LEVELS = 3;        // candidate / input digits
 constexpr int HEAD_UNROLL = 4;       // 16-B loads per thread per sample tile (16 Ki keys per 1024-thread tile)
 constexpr int BAR_GROUP_STRIDE = 64; // words between group counters (separate 256-B lines)
 constexpr int BAR_BASE = 8 * BAR_GROUP_STRIDE, BAR_ERR = BAR_BASE + BAR_GROUP_STRIDE;
-constexpr int BAR_WORDS = BAR_ERR + BAR_GROUP_STRIDE;  // u32 words of barrier state per ctx
+constexpr int BAR_TAIL = BAR_ERR + BAR_GROUP_STRIDE;  // u64 at this u32 index: k_finish tail (arrivals << 32 | keys)
+constexpr int BAR_WORDS = BAR_TAIL + BAR_GROUP_STRIDE;  // u32 words of barrier state per ctx
 constexpr uint32_t BAR_SPIN_LIMIT = 1u << 21;         // polls before a barrier gives up (seconds)
 constexpr uint32_t ERR_BARRIER = 64;
 
@@ -40,6 +41,7 @@ struct CoopArgs {
     uint32_t slack64;  // k_head early window (EarlyWindow); 0 = exact sample ranks
     u64 *zero2;        // k_finish: a second region to clear (the sample phase's slots)
     u64 zero2_words;
+    uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
 };
 
 // This wave's outstanding global accesses (atomics, write-through stores) are
@@ -119,7 +121,7 @@ __device__ __forceinline__ void grid_bar_finish(const GridBar &gb, const uint32_
 // device-coherent loads, and pick.
 template <int BLOCK>
 __device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool share, u64 *scratch,
-                                          const EarlyWindow *ew) {
+                                          const EarlyWindow *ew, u64 *cnt0 = nullptr) {
     constexpr int PER = NBINS / BLOCK;
     u64 h0[PER], h1[PER];
     const u64 *b0 = slot + NCOUNTS + threadIdx.x * PER;
@@ -128,7 +130,7 @@ __device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool sh
         h0[j] = __hip_atomic_load(b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         h1[j] = share ? 0ull : __hip_atomic_load(b0 + NBINS + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    pick_state<BLOCK, PER>(ss, h0, h1, share, scratch, ew);
+    pick_state<BLOCK, PER>(ss, h0, h1, share, scratch, ew, cnt0);
 }
 
 // The dense first digit of k_finish (nb <= NBINS / copies bins) is flushed
@@ -136,7 +138,7 @@ __device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool sh
 // same-address atomics); the pick loads the NBINS words once and sums them.
 template <int BLOCK>
 __device__ __forceinline__ void pick_slot_copies(SelState &ss, const u64 *slot, uint32_t nb, uint32_t copies,
-                                                 u64 *tmp /* NBINS u64 of LDS */, u64 *scratch) {
+                                                 u64 *tmp /* NBINS u64 of LDS */, u64 *scratch, u64 *cnt0) {
     constexpr int PER = NBINS / BLOCK;
 #pragma unroll
     for (int j = 0; j < PER; ++j)
@@ -153,7 +155,7 @@ __device__ __forceinline__ void pick_slot_copies(SelState &ss, const u64 *slot, 
         h0[j] = sum;
     }
     __syncthreads();
-    pick_state<BLOCK, PER>(ss, h0, h0, true, scratch, nullptr);
+    pick_state<BLOCK, PER>(ss, h0, h0, true, scratch, nullptr, cnt0);
 }
 
 // hist_flush into copy (blockIdx % copies) of a bins-wide histogram (target 0 only)
@@ -268,17 +270,18 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
 //     FIN_LDS_KEYS), every workgroup keeps its contiguous slice in LDS and the
 //     later digits scan LDS (each candidate level re-read the 21 MB of
 //     candidates: ~6 us a level at 2^30).
-//   * The first digit is 8 bits wide (FIN_D0; wider only when W > 30 needs
+//   * The first digit is 9 bits wide (FIN_D0; wider only when W > 30 needs
 //     it): every key of the domain lands in it, so every workgroup flushes
-//     nearly all of its bins -- 256 global atomics a workgroup, not 2048.  The
-//     later digits only see the keys of one bin.
+//     nearly all of its bins -- 512 global atomics a workgroup into 4 copies,
+//     not 2048 onto one.  The later digits only see the keys of one bin, and
+//     once that bin fits one workgroup's LDS, finish_tail ends the launch.
 //   * Slots come in two sets used by alternate launches (x.slots: this
 //     launch's, a.stats_zero: the other set, cleared here for the next one),
 //     and the sample phase's slots (x.zero2) are cleared here too: no barrier
 //     after the last level.
 constexpr int FIN_LDS_KEYS = 32768;  // LDS-resident keys per workgroup (128 KiB of dynamic LDS)
 constexpr int FIN_UNROLL = 4;        // 16-B loads in flight per thread (1024-thread workgroups: <= 128 VGPRs)
-constexpr uint32_t FIN_D0 = 8;
+constexpr uint32_t FIN_D0 = 9;  // [257, 512] bins used: ~12-25 K keys a bin from 6.3 M candidates
 
 __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPlan &plan, const uint4 &x, bool xr,
                                             uint32_t valid4) {
@@ -289,12 +292,179 @@ __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPla
     hist_add<DENSE_BLK>(lh, plan, x.w ^ X, valid4 & 8u);
 }
 
+// The tail of k_finish: once a level's picked bin holds <= FIN_LDS_KEYS keys,
+// the remaining digits need no more grid barriers.  Every workgroup appends
+// its slice's keys of that bin to x.tail (one reservation on the tail word's
+// low half), then arrives on its high half; the workgroup that arrives last
+// holds every key in the tail, loads them into its LDS and resolves the
+// remaining digits alone, with block barriers only.  (A grid level costs ~10
+// us: flush round trip + barrier + pick; the tail ~3 round trips.)  One CU
+// scans ~0.6 keys a clock (a 64-lane VALU op takes 4 clocks), so every pass
+// over keys here is lean: one scan of the slice (staged in LDS), 16-byte LDS
+// reads and one target in the finisher's levels.  Returns true on the
+// workgroup that finished.  Keys go to x.tail as order keys (xr: the domain
+// is the raw int32 input).
+constexpr uint32_t TAIL_STAGE = 2 * NBINS;  // keys a workgroup stages in LDS (the histogram's space)
+
+__device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, uint4 *res, u64 nk, bool xr,
+                            uint32_t (*lh)[NBINS], u64 *scratch) {
+    __shared__ uint32_t s_n, s_last, s_total;
+    __shared__ u64 s_off;
+    const uint32_t X = xr ? 0x80000000u : 0u;
+    const uint32_t W = ss.W, base = ss.base, done = ss.t[0].done, prefix = ss.t[0].prefix;
+    const uint32_t psh = W - done;  // done >= 1: a level was picked
+    const uint32_t nv = (uint32_t)((nk + 3) / 4);
+    u64 *ctl = reinterpret_cast<u64 *>(x.bar + BAR_TAIL);
+    uint32_t *stage = &lh[0][0];
+    const int lane = threadIdx.x & (WAVE - 1);
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    // one scan: the bin's keys appended to the LDS stage (ballot + mbcnt, one
+    // LDS atomic a wave and key slot that has any); a slice with more than
+    // TAIL_STAGE of them (skewed data) is written by a second scan instead
+    auto keep = [&](uint32_t key, bool valid) {
+        const bool m = valid && ((key - base) >> psh) == prefix;
+        const u64 b = __ballot(m);
+        if (b == 0) return;  // wave-uniform
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(&s_n, (uint32_t)__popcll(b));
+        at = __shfl(at, 0, WAVE);
+        const uint32_t i = at + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (m && i < TAIL_STAGE) stage[i] = key;
+    };
+    for (uint32_t v0 = 0; v0 < nv; v0 += DENSE_BLK) {  // wave-convergent
+        const uint32_t v = v0 + threadIdx.x;
+        uint4 q = make_uint4(0, 0, 0, 0);
+        uint32_t valid4 = 0;
+        if (v < nv) {
+            q = res[v];
+            const u64 e = 4ull * v;
+            valid4 = nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u;
+        }
+        keep(q.x ^ X, valid4 & 1u);
+        keep(q.y ^ X, valid4 & 2u);
+        keep(q.z ^ X, valid4 & 4u);
+        keep(q.w ^ X, valid4 & 8u);
+    }
+    __syncthreads();
+    const uint32_t n_mine = s_n;
+    if (threadIdx.x == 0)
+        s_off = n_mine ? __hip_atomic_fetch_add(ctl, (u64)n_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    __syncthreads();
+    const uint32_t off = (uint32_t)s_off;
+    if (n_mine <= TAIL_STAGE) {
+        for (uint32_t i = threadIdx.x; i < n_mine; i += DENSE_BLK)
+            if (off + i < (uint32_t)FIN_LDS_KEYS)
+                __hip_atomic_store(x.tail + off + i, stage[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {  // block-uniform: every key of the bin again, in a second scan
+        __shared__ uint32_t s_pos;
+        if (threadIdx.x == 0) s_pos = 0;
+        __syncthreads();
+        for (uint32_t v = threadIdx.x; v < nv; v += DENSE_BLK) {
+            const uint4 q = res[v];
+            const u64 e = 4ull * v;
+            const uint32_t valid4 = nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u;
+            const uint32_t k4[4] = {q.x ^ X, q.y ^ X, q.z ^ X, q.w ^ X};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (((valid4 >> j) & 1u) && ((k4[j] - base) >> psh) == prefix) {
+                    const uint32_t i = atomicAdd(&s_pos, 1u);
+                    if (off + i < (uint32_t)FIN_LDS_KEYS)
+                        __hip_atomic_store(x.tail + off + i, k4[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+        }
+    }
+    wait_mem();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const u64 old = __hip_atomic_fetch_add(ctl, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (uint32_t)(old >> 32) == gridDim.x - 1u;
+        s_total = (uint32_t)old;
+        if (s_last) __hip_atomic_store(ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next select
+    }
+    __syncthreads();
+    KTH_STAMP(a, 5);
+    if (!s_last) return false;
+    const uint32_t total = s_total;
+    if (total > (uint32_t)FIN_LDS_KEYS) {  // cannot happen: the bin's reduced count was checked
+        if (threadIdx.x == 0) {
+            ss.error = 32;
+            ss.mode = MODE_DONE;
+        }
+        __syncthreads();
+        return true;
+    }
+    // 16-byte device-coherent loads, FIN_UNROLL in flight per thread (a
+    // per-key loop waited one round trip per key); the last vector is padded
+    // with a key of another bin of the entry digit, which matches no later
+    // prefix either
+    const uint32_t nq = (total + 3) / 4;
+    {
+        constexpr int TU = FIN_LDS_KEYS / 4 / DENSE_BLK;
+        static_assert(TU % FIN_UNROLL == 0, "tail loads in FIN_UNROLL batches");
+        const CoherentBuf tb(x.tail, FIN_LDS_KEYS * 4);
+        for (int u0 = 0; u0 < TU; u0 += FIN_UNROLL) {
+            if ((uint32_t)(u0 * DENSE_BLK) >= nq) break;  // block-uniform
+            uint4 q[FIN_UNROLL];
+#pragma unroll
+            for (int u = 0; u < FIN_UNROLL; ++u) {
+                const uint32_t v = (u0 + u) * DENSE_BLK + threadIdx.x;
+                q[u] = v < nq ? tb.load16(v * 16u) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < FIN_UNROLL; ++u) {
+                const uint32_t v = (u0 + u) * DENSE_BLK + threadIdx.x;
+                if (v == total / 4 && (total & 3u)) {
+                    const uint32_t pad = base + ((prefix ^ 1u) << psh);
+                    if ((total & 3u) <= 1) q[u].y = pad;
+                    if ((total & 3u) <= 2) q[u].z = pad;
+                    q[u].w = pad;
+                }
+                res[(u0 + u) * DENSE_BLK + threadIdx.x] = q[u];
+            }
+        }
+        __syncthreads();
+    }
+    KTH_STAMP(a, 6);
+    // the remaining digits in LDS, one target (pick_state ends with a barrier)
+    constexpr int PER = NBINS / DENSE_BLK;
+    for (int it = 0; ss.mode == MODE_CAND || ss.mode == MODE_FULL; ++it) {  // block-uniform
+        (void)it;
+        const uint32_t dn = ss.t[0].done, pf = ss.t[0].prefix, d = digit_bits(ss, dn);
+        const uint32_t msh = W - dn, sh = W - dn - d, mask = (1u << d) - 1u;
+        for (int i = threadIdx.x; i < NBINS / 4; i += DENSE_BLK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        auto add = [&](uint32_t key) {
+            const uint32_t v = key - base;
+            if ((v >> msh) == pf) atomicAdd(&lh[0][(v >> sh) & mask], 1u);  // msh < 32: dn >= 1
+        };
+        for (uint32_t v = threadIdx.x; v < nq; v += DENSE_BLK) {
+            const uint4 q = res[v];
+            add(q.x);
+            add(q.y);
+            add(q.z);
+            add(q.w);
+        }
+        __syncthreads();
+        u64 h0[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) h0[j] = lh[0][threadIdx.x * PER + j];
+        pick_state<DENSE_BLK, PER>(ss, h0, h0, true, scratch, nullptr);
+#ifdef KTH_STAMPS_BUILD
+        if (it < 2) KTH_STAMP(a, 1 + it);  // diagnostic only: the finisher overwrites its own early stamps
+#endif
+    }
+    KTH_STAMP(a, 3);
+    return true;
+}
+
 __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
     __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
     extern __shared__ uint4 res[];  // FIN_LDS_KEYS / 4 entries (dynamic)
     __shared__ uint32_t s_base[8];
+    __shared__ u64 s_cnt0;
     KTH_STAMP(a, 0);
     GridBar gb = grid_bar_init(x.bar, s_base);
     for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
@@ -317,7 +487,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         b0 = min((u64)blockIdx.x * per, count);
         nk = min(per, count - b0);
     }
-    bool ok = true;
+    bool ok = true, tail = false;
     for (int L = 0; L < FIN_LEVELS; ++L) {
         const uint32_t mode = ss.mode;
         if (mode != MODE_CAND && mode != MODE_FULL) break;  // block-uniform
@@ -396,13 +566,22 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         grid_sync(gb, s_base, ok);
         if (L == 0) KTH_STAMP(a, 3);
         if (copies > 1)
-            pick_slot_copies<DENSE_BLK>(ss, slot, nb, copies, reinterpret_cast<u64 *>(&lh[0][0]), scratch);
+            pick_slot_copies<DENSE_BLK>(ss, slot, nb, copies, reinterpret_cast<u64 *>(&lh[0][0]), scratch, &s_cnt0);
         else
-            pick_slot<DENSE_BLK>(ss, slot, share, scratch, nullptr);
+            pick_slot<DENSE_BLK>(ss, slot, share, scratch, nullptr, &s_cnt0);
         KTH_STAMP(a, 4 + L);
+        // a small bin left: the last workgroup to arrive finishes alone (block-uniform)
+        if (resident && (ss.mode == MODE_CAND || ss.mode == MODE_FULL) && s_cnt0 <= (u64)FIN_LDS_KEYS) {
+            tail = true;
+            break;
+        }
     }
     grid_bar_finish(gb, s_base);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    bool writer = blockIdx.x == 0;
+    if (tail) {
+        writer = finish_tail(a, ss, x, res, nk, xr, lh, scratch);
+    }
+    if (writer && threadIdx.x == 0) {
         SelState o = ss;
         const uint32_t berr = __hip_atomic_exchange(x.bar + BAR_ERR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((!ok || berr) && !o.error) o.error = ERR_BARRIER;

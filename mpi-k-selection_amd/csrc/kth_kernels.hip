@@ -169,10 +169,10 @@ __device__ __forceinline__ void early_window(SelState &s, const EarlyWindow &e, 
 // Pick every live target's next digit from a histogram the caller holds in
 // registers (thread i owns bins [i*PER, i*PER + PER) of target t in h[t];
 // `share`: target 1 reads target 0's histogram).  Thread 0 updates ss; ends
-// with a barrier.
+// with a barrier.  cnt0 (LDS, optional): keys in target 0's picked bin.
 template <int BLOCK, int PER>
 __device__ __forceinline__ void pick_state(SelState &ss, const u64 (&h0)[PER], const u64 (&h1)[PER], bool share,
-                                           u64 *scratch, const EarlyWindow *ew = nullptr) {
+                                           u64 *scratch, const EarlyWindow *ew = nullptr, u64 *cnt0 = nullptr) {
     const uint32_t mode = ss.mode;
     const bool live = mode == MODE_SAMPLE || mode == MODE_CAND || mode == MODE_FULL;
     bool want[2];
@@ -201,6 +201,7 @@ __device__ __forceinline__ void pick_state(SelState &ss, const u64 (&h0)[PER], c
         }
         resolve(ss);
         if (ew && want[0] == ss.t[0].active && want[1] == ss.t[1].active) early_window(ss, *ew, cnt[1]);
+        if (cnt0) *cnt0 = want[0] ? cnt[0] : ~0ull;
     }
     __syncthreads();
 }
