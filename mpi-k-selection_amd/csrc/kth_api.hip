@@ -81,7 +81,7 @@ constexpr int MAX_EVENTS = 4 * 2048;
 
 struct kth_ctx {
     int device = 0;
-    int main_grid[3] = {0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
+    int main_grid[5] = {0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
     bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
@@ -99,6 +99,8 @@ struct kth_ctx {
     u64 sample_cap = 0;
     uint32_t *cand = nullptr;
     u64 cand_cap = 0;
+    uint32_t *cand_rows = nullptr;  // k_main<3/4>: each candidate's 1024-key row (top-k)
+    u64 cand_rows_cap = 0;
     int32_t *staging = nullptr;
     u64 staging_cap = 0;
     u64 *topk = nullptr;  // top-k chunk counts, bases, [need, error]
@@ -384,6 +386,18 @@ int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
     return launch_check();
 }
 
+// The streaming pass, plain (tflag 0) or with the top-k records of k_main<tflag>.
+void launch_main(kth_ctx *c, const StepArgs &a, int tflag, uint32_t *tflags) {
+    const int g = c->main_grid[tflag];
+    switch (tflag) {
+    case 1: kth::k_main<1><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr); break;
+    case 2: kth::k_main<2><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr); break;
+    case 3: kth::k_main<3><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows); break;
+    case 4: kth::k_main<4><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows); break;
+    default: kth::k_main<0><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr); break;
+    }
+}
+
 // The main pass + candidate levels + result, shared by the single-GPU window
 // path.  Expects the window state in st[0] and the last sample digit's
 // histogram in islot(0).
@@ -414,12 +428,7 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
         a.keys = keys;
         a.n_local = (u64)n;
         ev_main(c);
-        if (tflag == 1)
-            kth::k_main<1><<<c->main_grid[1], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
-        else if (tflag == 2)
-            kth::k_main<2><<<c->main_grid[2], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
-        else
-            kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+        launch_main(c, a, tflag, tflags);
         ev_main(c);
         // decide + candidate (or fallback) levels + answer in one launch
         a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), nullptr, nullptr);
@@ -453,12 +462,7 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     a.keys = keys;
     a.n_local = (u64)n;
     ev_main(c);
-    if (tflag == 1)
-        kth::k_main<1><<<c->main_grid[1], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
-    else if (tflag == 2)
-        kth::k_main<2><<<c->main_grid[2], kth::BLK, 0, c->stream>>>(a, c->cand, tflags);
-    else
-        kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+    launch_main(c, a, tflag, tflags);
     ev_main(c);
     // decide + candidate (or fallback) levels.  The grids cover the fallback
     // (whole input); in the common case only the WGs the candidates need run.
@@ -614,11 +618,13 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // holds 512 / alloc(VGPR) waves, MI355X_MICROARCH.md register files);
             // the top-k variants keep more keys live and may allocate more VGPRs.
             // hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports here.
-            const void *fns[3] = {reinterpret_cast<const void *>(kth::k_main<0>),
+            const void *fns[5] = {reinterpret_cast<const void *>(kth::k_main<0>),
                                   reinterpret_cast<const void *>(kth::k_main<1>),
-                                  reinterpret_cast<const void *>(kth::k_main<2>)};
+                                  reinterpret_cast<const void *>(kth::k_main<2>),
+                                  reinterpret_cast<const void *>(kth::k_main<3>),
+                                  reinterpret_cast<const void *>(kth::k_main<4>)};
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
-            for (int v = 0; v < 3; ++v) {
+            for (int v = 0; v < 5; ++v) {
                 int per = 4;
                 hipFuncAttributes fa;
                 if (hipFuncGetAttributes(&fa, fns[v]) == hipSuccess && fa.numRegs > 0) {
@@ -688,6 +694,7 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->islots) (void)hipFree(c->islots);
     if (c->sample) (void)hipFree(c->sample);
     if (c->cand) (void)hipFree(c->cand);
+    if (c->cand_rows) (void)hipFree(c->cand_rows);
     if (c->staging) (void)hipFree(c->staging);
     if (c->topk) (void)hipFree(c->topk);
     if (c->d_status) (void)hipFree(c->d_status);
@@ -881,14 +888,31 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     u64 head = ((16u - (uint32_t)(reinterpret_cast<uintptr_t>(d_keys) & 15u)) & 15u) >> 2;
     if (head > (u64)n) head = (u64)n;
     const u64 nfull = (((u64)n - head) >> 2) / ((u64)kth::BLK * kth::MAIN_UNROLL);
-    const u64 fwords = 4 + nfull;
-    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2 + (fwords + 1) / 2;
+    // k_main's top-k records (only on the window path, n > RADIX_MAX_N):
+    //   16-byte aligned keys: per wave-row counts + candidate rows, and the
+    //   count pass loads no tile k_main covered (tf 3 / 4) -- unless k is so
+    //   small that the rows holding output are a few per cent (k * 64 Ki <=
+    //   n: one flag bit per row, the count pass loads only flagged tiles,
+    //   tf 1 / 2; measured ~equal there, and it needs no alignment)
+    const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
+    const bool window = n > RADIX_MAX_N;
+    const bool few = (u64)k * kth::TK_TILE * 64 <= (u64)n;
+    const int tf = (aligned && window && !few)             ? (largest ? 4 : 3)
+                   : (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1)
+                                                             : 0;
+    const u64 ncov = tf >= 3 ? nfull * kth::MAIN_UNROLL : 0;  // tiles = k_main rows (head == 0)
+    const u64 fwords = 4 + (tf >= 3 ? ncov * (kth::BLK / kth::WAVE) : nfull);
+    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2 + (fwords + 3) / 2 + 1;
     KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
-    uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + (words - (fwords + 1) / 2));
+    // tflags 16-byte aligned (k_topk_count reads the wave-row words as uint4)
+    const u64 foff = words - (fwords + 3) / 2 - 1;  // one spare u64: rounded up to 16 bytes
+    uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + (foff + (foff & 1)));
     HIP_TRY(hipMemsetAsync(tflags, 0, 16, c->stream));  // window header: not valid until k_main<TF> runs
+    if (tf >= 3) {
+        KTH_TRY(reserve_cand(c, n));
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->cand_rows), &c->cand_rows_cap, c->cand_cap));
+    }
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
-    // tile flags from the streaming pass pay off when few 1024-key tiles can hold output
-    const int tf = (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1) : 0;
     int64_t rank = largest ? n - k + 1 : k;
     if (c->fault_topk_rank && n > 1) rank = rank < n ? rank + 1 : rank - 1;
     KTH_TRY(select_async(c, d_keys, n, rank, nullptr, c->d_status, tf, tflags));
@@ -896,16 +920,50 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     const uint32_t flip = largest ? 0xFFFFFFFFu : 0u;
     u64 *toff = c->topk, *bsum = toff + ntiles, *bbase = bsum + 2 * nblk, *meta = bbase + 2 * nblk;
     uint32_t *tcnt = reinterpret_cast<uint32_t *>(meta + 2);
-    const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
+    const SelState *sel_st = c->st + c->last_state;
     // count and write passes: one wave per 64 tiles
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
-    if (aligned)
-        kth::k_topk_count<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
-                                                                     tflags, head, nfull);
-    else
-        kth::k_topk_count<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
-                                                                     tflags, head, nfull);
+    if (tf >= 3) {
+        kth::k_topk_count<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+                                                                          tcnt, tflags, head, nfull, sel_st, ncov);
+        kth::k_topk_cands<<<c->num_cu * 8, kth::TK_BLOCK, 0, c->stream>>>(
+            c->cand, c->cand_rows, cand_count(c), c->cand_cap / 4, c->d_status, flip, tcnt, tflags, sel_st);
+    } else if (aligned) {
+        kth::k_topk_count<true, false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+                                                                           tcnt, tflags, head, nfull, sel_st, 0);
+    } else {
+        kth::k_topk_count<false, false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+                                                                            tcnt, tflags, head, nfull, sel_st, 0);
+    }
+    if (getenv("KTH_TOPK_DEBUG")) {  // diagnostic: tile counts against a host recount
+        (void)hipStreamSynchronize(c->stream);
+        std::vector<uint32_t> h_t(ntiles), h_f(4), h_k(n);
+        std::vector<int32_t> h_v(2);
+        SelState h_s;
+        (void)hipMemcpy(h_t.data(), tcnt, ntiles * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h_f.data(), tflags, 16, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h_v.data(), c->d_status, 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&h_s, sel_st, sizeof h_s, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h_k.data(), d_keys, (size_t)n * 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "kth-topk-debug tf %d ncov %llu v %d err %d lo %d hi %d valid %u ovf %llu path %u\n", tf,
+                (unsigned long long)ncov, h_v[0], h_v[1], (int32_t)h_f[0], (int32_t)h_f[1], h_f[2],
+                (unsigned long long)h_s.cnt[4], h_s.path);
+        int shown = 0;
+        for (u64 t = 0; t < ntiles && shown < 8; ++t) {
+            uint32_t b = 0, e = 0;
+            for (u64 i = t * 1024; i < std::min<u64>((u64)n, t * 1024 + 1024); ++i) {
+                const int32_t x = (int32_t)h_k[i];
+                b += largest ? x > h_v[0] : x < h_v[0];
+                e += x == h_v[0];
+            }
+            if ((b | e << 16) != (h_t[t] & 0x7FFFFFFFu)) {
+                fprintf(stderr, "  tile %llu: got b %u e %u want b %u e %u\n", (unsigned long long)t, h_t[t] & 0xFFFF,
+                        h_t[t] >> 16, b, e);
+                ++shown;
+            }
+        }
+    }
     kth::k_topk_reduce<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, bsum);
     // a bracket failure (counts that do not hold the k-th) lands in the select's
     // state, where kth_ctx_last_stats reports it as .error
@@ -1017,7 +1075,7 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
-    kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr);
+    kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr);
     ev_main(c);
     c->dist_level_next = 0;
     KTH_TRY(launch_check());

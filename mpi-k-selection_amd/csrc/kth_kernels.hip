@@ -566,25 +566,39 @@ __device__ __forceinline__ void put_cand(uint32_t *p, uint32_t x) {
     __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ROWS (k_main<3/4>, top-k): every candidate also carries the 1024-key row it
+// came from (wave-uniform per key slot), staged in the region's upper half and
+// written to rows_out beside it; ~0u = a row outside k_main's full tiles.
+template <bool ROWS = false>
 struct Stager {
+    static constexpr uint32_t CAP = ROWS ? WREG / 2 : WREG;  // keys the region holds
     uint32_t *reg;       // this wave's LDS region (WREG words)
     uint32_t wfill;      // wave-uniform fill of the region
     u64 winside;         // wave-uniform count of candidates seen
     u64 *cand_count, *acc, cap;
     uint32_t *cand_out;
+    uint32_t *rows_out;  // ROWS only
+
+    // the region's first `cnt` keys (and rows) to candidates [g, g + cnt)
+    __device__ __forceinline__ void put(u64 g, uint32_t cnt) const {
+        const int lane = threadIdx.x & (WAVE - 1);
+        for (uint32_t i = lane; i < cnt; i += WAVE)
+            if (g + i < cap) {
+                put_cand(&cand_out[g + i], reg[i]);
+                if (ROWS) put_cand(&rows_out[g + i], reg[CAP + i]);
+            }
+    }
 
     __device__ __forceinline__ void flush() {
         __builtin_amdgcn_wave_barrier();
-        const int lane = threadIdx.x & (WAVE - 1);
         const u64 g = reserve_cands(cand_count, acc, cap, wfill);
-        for (uint32_t i = lane; i < wfill; i += WAVE)
-            if (g + i < cap) put_cand(&cand_out[g + i], reg[i]);
+        put(g, wfill);
         __builtin_amdgcn_wave_barrier();
         wfill = 0;
     }
 
     // One key slot of the wave: `in` = this lane's key is a candidate.
-    __device__ __forceinline__ void slot(uint32_t key, bool in) {
+    __device__ __forceinline__ void slot(uint32_t key, bool in, uint32_t row = ~0u) {
         const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
 #ifdef KTH_DIAG_NOSTAGE
         if (B == 0x123456789ull) {  // diagnostic build only: measures the staging cost
@@ -592,10 +606,13 @@ struct Stager {
         if (B) {  // wave-uniform
 #endif
             const uint32_t nb = (uint32_t)__popcll(B);
-            if (wfill + nb > (uint32_t)WREG) flush();
+            if (wfill + nb > CAP) flush();
             const uint32_t below =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
-            if (in) reg[wfill + below] = key;
+            if (in) {
+                reg[wfill + below] = key;
+                if (ROWS) reg[CAP + wfill + below] = row;
+            }
             wfill += nb;
             winside += nb;
         }
@@ -606,9 +623,27 @@ struct Stager {
 // keys are the raw int32 words: signed compares against the signed window
 // bounds order them exactly like the order-preserving keys (no per-key xor);
 // only a staged candidate is converted.
-template <int K, bool FULL>
+// DPP-shifted copy of x (0 where the shift has no source lane), for wave scans
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+
+// k_main<3/4>'s per-row tallies of one tile (this lane): #beyond (#<lo for
+// RW 3, #>hi for 4) of row u in r[u] (one add-with-carry a key).  Counted
+// where the compares are made (a second set of compares elsewhere kept compare
+// masks live in SGPRs and made the loop spill them).
+struct RowAcc {
+    uint32_t r[8];
+};
+
+// ROWS: key j lies in row row0 + j / 4 (row0 = ~0u: not tracked).  RW 3 / 4:
+// tally rows into ra (FULL tiles of 32 keys per lane only).
+template <int K, bool FULL, bool ROWS, int RW = 0>
 __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t valid, int32_t slo, int32_t shi,
-                                          uint32_t &clt, uint32_t &ceqlo, uint32_t &ceqhi, Stager &st) {
+                                          uint32_t &clt, uint32_t &ceqlo, uint32_t &ceqhi, Stager<ROWS> &st,
+                                          uint32_t row0 = ~0u, RowAcc *ra = nullptr) {
+    static_assert(RW == 0 || (FULL && K == 32), "row tallies cover a full tile's 8 rows");
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const int32_t x = (int32_t)xw[j];
@@ -616,7 +651,10 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
         clt += (ok & (x < slo)) ? 1u : 0u;
         ceqlo += (ok & (x == slo)) ? 1u : 0u;
         ceqhi += (ok & (x == shi)) ? 1u : 0u;
-        st.slot((uint32_t)x ^ 0x80000000u, ok & (x > slo) & (x < shi));
+        if constexpr (RW != 0) {
+            ra->r[j / 4] += (RW == 3 ? x < slo : x > shi) ? 1u : 0u;
+        }
+        st.slot((uint32_t)x ^ 0x80000000u, ok & (x > slo) & (x < shi), row0 == ~0u ? ~0u : row0 + (uint32_t)(j / 4));
     }
 }
 
@@ -626,17 +664,31 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 // ((uint8_t *)(tflags + 4))[4 * tile + wave]; and the window as tflags[0..2] =
 // {lo, hi, 1} (signed).  A row with no bit set in any wave holds no output key
 // of the top-k when its k-th lies inside the window.
+// 3 / 4 (k smallest / largest, k > n / 1024): per full tile, row u and wave,
+// one word #beyond (#<lo for 3, #>hi for 4; <= 256 keys a wave-row), or'ed
+// with TK_RECOUNT when the wave-tile holds a key equal to lo or hi, at
+// tflags[4 + (row * 4 + wave)], row = tile * U + u; and every candidate's row
+// in cand_rows.  With the candidates these give every unmarked row's #better /
+// #equal for any k-th inside the window, so the top-k re-reads only marked
+// rows to count (k_topk_count<.., META>).
+constexpr uint32_t TK_RECOUNT = 1u << 31;
 static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot in a byte");
 static_assert(BLK / WAVE == 4, "k_main<TF> stores one flag byte per wave, four per tile (tk_row_flagged's mask)");
 template <int TF>
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out,
-                                              uint32_t *__restrict__ tflags) {
+                                              uint32_t *__restrict__ tflags, uint32_t *__restrict__ cand_rows) {
     constexpr int U = MAIN_UNROLL, S = MAIN_SUB, K = 4 * S;
+#ifdef KTH_DIAG_NOROWS  // diagnostic builds only (wrong top-k results): cost of the row tags
+    constexpr bool ROWS = false;
+#else
+    constexpr bool ROWS = TF >= 3;
+#endif
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
     __shared__ uint32_t region[BLK / WAVE][WREG];
     __shared__ u64 red[6][BLK / WAVE];
+    __shared__ uint32_t rowx[BLK / WAVE][4];  // k_main<3/4>: a wave's row sums in transit
     KTH_STAMP(a, 0);
     const uint32_t *p = reinterpret_cast<const uint32_t *>(a.keys);
     const u64 n = a.n_local;
@@ -653,6 +705,9 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         const uint4 *src = v + t * tile + threadIdx.x;
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
+        // (The compiler issues 2 loads, waits for the first, then issues the
+        // other U-2.  A sched_barrier here that sends all U first measured
+        // slower: k_main 640 -> 685 us.)
     };
     // (Issuing the first tile's loads before the advance made the pass slower,
     // 656 vs 642 us: the advance's histogram loads then wait behind them.)
@@ -669,11 +724,13 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             tflags[2] = 1u;
         }
     }
-    Stager st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out};
+    Stager<ROWS> st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out, cand_rows};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
 
     // a tile is consumed in groups of 4 * MAIN_SUB keys
-    auto scan_tile = [&](const uint4 (&x)[U]) {
+    constexpr int RW = TF >= 3 ? TF : 0;
+    auto scan_tile = [&](const uint4 (&x)[U], u64 t, RowAcc &ra) {
+        static_assert(RW == 0 || U == S, "row tallies: one key group per tile");
 #pragma unroll
         for (int h = 0; h < U / S; ++h) {
             uint32_t kk[K];
@@ -684,11 +741,19 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 kk[4 * u + 2] = x[h * S + u].z;
                 kk[4 * u + 3] = x[h * S + u].w;
             }
-            scan_keys<K, true>(kk, 0xFFFFFFFFu, slo, shi, clt, ceqlo, ceqhi, st);
+            scan_keys<K, true, ROWS, RW>(kk, 0xFFFFFFFFu, slo, shi, clt, ceqlo, ceqhi, st,
+                                         ROWS ? (uint32_t)(t * U + h * S) : ~0u, &ra);
         }
     };
-    auto flag_tile = [&](const uint4 (&x)[U], u64 t) {
-        if constexpr (TF != 0) {
+    // (e0: this lane's ceqlo + ceqhi before the tile; a change = a key on an edge)
+    // TF 3 / 4: a wave-tile's row words are stored one tile later, after the
+    // next tile's loads are issued (stored at once, the store's data register
+    // was reused by the next tile's load addresses and the compiler made the
+    // loads wait for the store: +70 us a pass); pend_at = word index (~0: none).
+    u64 pend_at = ~0ull;
+    uint32_t pend_word = 0;
+    auto flag_tile = [&](const uint4 (&x)[U], u64 t, const RowAcc &ra, uint32_t e0) {
+        if constexpr (TF == 1 || TF == 2) {
             // bit u of the wave's byte: some key of row u (the tile's u-th run of
             // 4 * BLK keys) in this wave's part is <= hi (TF 1) / >= lo (TF 2)
             uint32_t rows = 0;
@@ -700,14 +765,63 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             }
             if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = (uint8_t)rows;
         }
+#ifdef KTH_DIAG_NOROWW  // diagnostic builds only (wrong top-k results): cost of the row words
+        if constexpr (TF >= 5) {
+#else
+        if constexpr (TF >= 3) {
+#endif
+            static_assert(U == 8, "k_main<3/4> packs four rows' counts into each of two words");
+            // #beyond per row: a lane holds <= 4 keys of a row, so rows 0-3 / 4-7
+            // fit 8-bit fields of b0 / b1 over a 32-lane half (<= 128); two DPP
+            // half-wave scans.  The halves' sums go through the wave's LDS words
+            // to lanes 0..7 (readlanes into SGPRs made the loop spill SGPRs).  A
+            // wave-tile with a key on a window edge (uniform keys: never) is
+            // marked TK_RECOUNT instead: the count pass reads those rows (per-row
+            // edge tallies here made the loop spill SGPRs too).
+            // rows 0-3 / 4-7 into the 8-bit fields of b0 / b1 (a lane's row count <= 4)
+            uint32_t b0 = ra.r[0] | ra.r[1] << 8 | ra.r[2] << 16 | ra.r[3] << 24;
+            uint32_t b1 = ra.r[4] | ra.r[5] << 8 | ra.r[6] << 16 | ra.r[7] << 24;
+            auto half_scan = [](uint32_t c) {
+                c += dpp_add<0x111>(c);       // row_shr:1
+                c += dpp_add<0x112>(c);       // row_shr:2
+                c += dpp_add<0x114>(c);       // row_shr:4
+                c += dpp_add<0x118>(c);       // row_shr:8
+                c += dpp_add<0x142, 0xA>(c);  // row_bcast:15 -> lanes 31, 63: the halves' sums
+                return c;
+            };
+#ifndef KTH_DIAG_NOSCAN  // diagnostic builds only (wrong top-k results)
+            b0 = half_scan(b0);
+            b1 = half_scan(b1);
+#endif
+            uint32_t *rx = rowx[wid];
+            if ((lane & 31) == 31) {
+                rx[lane >> 5] = b0;
+                rx[2 + (lane >> 5)] = b1;
+            }
+            const uint32_t mark = __builtin_amdgcn_ballot_w64(ceqlo + ceqhi != e0) != 0 ? TK_RECOUNT : 0u;
+            __builtin_amdgcn_wave_barrier();  // a wave's LDS accesses are in order
+            if (lane < U) {
+                const uint32_t q = lane < 4 ? 0u : 2u, sh = 8 * (lane & 3);
+                const uint32_t word = ((rx[q] >> sh) & 0xFFu) + ((rx[q + 1] >> sh) & 0xFFu);
+                pend_word = word | mark;
+                pend_at = 4 + ((t * U + lane) * (BLK / WAVE) + wid);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
     };
     // every load of a tile issued before any use
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
+        RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
+        const uint32_t e0 = ceqlo + ceqhi;
         load_tile(x, t);
-        scan_tile(x);
-        flag_tile(x, t);
+        if constexpr (TF >= 3)
+            if (pend_at != ~0ull) tflags[pend_at] = pend_word;  // the previous tile's words (lanes 0..U-1)
+        scan_tile(x, t, ra);
+        flag_tile(x, t, ra, e0);
     }
+    if constexpr (TF >= 3)
+        if (pend_at != ~0ull) tflags[pend_at] = pend_word;
     // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;
     if (blockIdx.x == (uint32_t)(nfull % gridDim.x))
@@ -769,8 +883,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     if (st.wfill) {  // this wave's final region, at its share of the reservation
         u64 g = red[5][0];
         for (int w = 0; w < wid; ++w) g += red[4][w];
-        for (uint32_t i = lane; i < st.wfill; i += WAVE)
-            if (g + i < a.cap) put_cand(&cand_out[g + i], st.reg[i]);
+        st.put(g, st.wfill);
     }
     KTH_STAMP(a, 5);
 }

@@ -60,21 +60,47 @@ __device__ __forceinline__ bool tk_row_flagged(const uint32_t *fw, u64 r) {
     return (fw[r / MAIN_UNROLL] & (0x01010101u << (r % MAIN_UNROLL))) != 0u;
 }
 
-template <bool ALIGNED>
+// META (after k_main<3/4>, 16-byte aligned keys): the first ncov tiles are
+// k_main's rows; when v lies inside the window and no candidate was dropped
+// (meta_ok), an unmarked row holds no key equal to lo or hi, so its #better is
+// the sum of its four wave-row words (#<lo, or #>hi for largest) and k_topk_cands
+// adds the candidates' share: no key of it is loaded.  Marked rows
+// (TK_RECOUNT) are counted from the input.
+__device__ __forceinline__ bool tk_meta_ok(const uint32_t *tflags, const int32_t *d_v, const SelState *st) {
+    return tflags[2] == 1u && d_v[0] >= (int32_t)tflags[0] && d_v[0] <= (int32_t)tflags[1] && st->cnt[C_OVF] == 0;
+}
+
+// a tile count word: #better | #equal << 16, plus TK_RECOUNT (bit 31) on a
+// META tile counted from the input (k_topk_cands then leaves it alone)
+__device__ __forceinline__ uint32_t tk_better_of(uint32_t c) { return c & 0xFFFFu; }
+__device__ __forceinline__ uint32_t tk_equal_of(uint32_t c) { return (c >> 16) & 0x7FFFu; }
+
+template <bool ALIGNED, bool META>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          uint32_t *__restrict__ tcnt,
-                                                         const uint32_t *__restrict__ tflags, u64 head, u64 nfull) {
+                                                         const uint32_t *__restrict__ tflags, u64 head, u64 nfull,
+                                                         const SelState *__restrict__ st, u64 ncov) {
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
-    const bool skip_ok = tflags[2] == 1u && (flip == 0u ? d_v[0] <= (int32_t)tflags[1] : d_v[0] >= (int32_t)tflags[0]);
+    const bool skip_ok =
+        !META && tflags[2] == 1u && (flip == 0u ? d_v[0] <= (int32_t)tflags[1] : d_v[0] >= (int32_t)tflags[0]);
+    const bool meta_ok = META && tk_meta_ok(tflags, d_v, st);
+    const uint32_t mark = meta_ok ? TK_RECOUNT : 0u;
     const uint32_t *fw = tflags + 4;
     // each wave takes 64 tiles at a time: lane l tests tile tg + l's flags, the
     // wave then streams only the tiles that may hold output
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE) * WAVE; tg < ntiles; tg += nw * WAVE) {
         const u64 tl = tg + lane;
         bool act = tl < ntiles;
+        if (act && meta_ok && tl < ncov) {
+            const uint4 w = reinterpret_cast<const uint4 *>(fw)[tl];
+            if (((w.x | w.y | w.z | w.w) & TK_RECOUNT) == 0u) {
+                tcnt[tl] = w.x + w.y + w.z + w.w;  // <= 1024
+                act = false;
+            }
+        }
         if (act && skip_ok && tl * TK_TILE >= head) {
             const u64 b0 = tl * TK_TILE, last = (b0 + TK_TILE < n ? b0 + TK_TILE : n) - 1;
             const u64 ra = (b0 - head) / TK_MAIN_ROW, rb = (last - head) / TK_MAIN_ROW;
@@ -126,10 +152,34 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
             c1 = wave_sum32(c1);
             c2 = wave_sum32(c2);
             if (lane == 0) {
-                tcnt[t1] = c1;
-                if (two) tcnt[t2] = c2;
+                tcnt[t1] = c1 | mark;
+                if (two) tcnt[t2] = c2 | mark;
             }
         }
+    }
+}
+
+// Pass 1b (META): the candidates' share of their rows' counts (one atomic per
+// candidate that is better than or equal to v; rows past ncov were counted
+// from the input and carry row ~0u).
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restrict__ cand,
+                                                         const uint32_t *__restrict__ rows,
+                                                         const u64 *__restrict__ cand_count, u64 cap,
+                                                         const int32_t *__restrict__ d_v, uint32_t flip,
+                                                         uint32_t *__restrict__ tcnt,
+                                                         const uint32_t *__restrict__ tflags,
+                                                         const SelState *__restrict__ st) {
+    if (!tk_meta_ok(tflags, d_v, st)) return;
+    const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
+    const u64 m = min(*cand_count, cap);
+    for (u64 i = (u64)blockIdx.x * TK_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * TK_BLOCK) {
+        const uint32_t r = rows[i];
+        if (r == ~0u || (tcnt[r] & TK_RECOUNT)) continue;  // outside k_main's rows / counted from the input
+        const uint32_t u = cand[i];
+        if (tk_better(u, uv, flip))
+            atomicAdd(&tcnt[r], 1u);
+        else if (u == uv)
+            atomicAdd(&tcnt[r], 0x10000u);
     }
 }
 
@@ -141,7 +191,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_reduce(const uint32_t *__rest
     for (int j = 0; j < 16; ++j)
         if (t0 + j < ntiles) {
             const uint32_t c = tcnt[t0 + j];
-            s += (c & 0xFFFFu) | ((u64)(c >> 16) << 32);
+            s += tk_better_of(c) | ((u64)tk_equal_of(c) << 32);
         }
     __shared__ u64 wsum[TK_BLOCK / WAVE];
     u64 tot;
@@ -196,7 +246,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t c = t0 + j < ntiles ? tcnt[t0 + j] : 0u;
-        v[j] = (c & 0xFFFFu) | ((u64)(c >> 16) << 32);
+        v[j] = tk_better_of(c) | ((u64)tk_equal_of(c) << 32);
         s += v[j];
     }
     __shared__ u64 wsum[TK_BLOCK / WAVE];
@@ -240,7 +290,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
             bb_l = bbase[2 * blk] + (off & 0xFFFFFFFFull);
             be_l = bbase[2 * blk + 1] + (off >> 32);
         }
-        const bool act = (c_l & 0xFFFFu) != 0 || ((c_l >> 16) != 0 && be_l < need);
+        const bool act = tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need);
         u64 todo = __ballot(act);
         while (todo) {
             const int src = __builtin_ctzll(todo);
@@ -251,9 +301,9 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
             const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
-            const u64 ce = c >> 16;
+            const u64 ce = tk_equal_of(c);
             const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
-            const uint32_t total = (c & 0xFFFFu) + (uint32_t)take_e;  // this tile's output keys
+            const uint32_t total = tk_better_of(c) + (uint32_t)take_e;  // this tile's output keys
             const u64 start = bb + (be < need ? be : need);            // and where they go
             const u64 i0 = t * TK_TILE + (u64)lane * TK_KPL;
             uint32_t x[TK_KPL];

@@ -179,3 +179,30 @@ def test_topk_bracket_failure_is_reported(gpu):
     vals, idx = _run(gpu, d, n, k, False)  # a normal ctx: no error
     assert gpu.stats()["error"] == 0
     np.testing.assert_array_equal(idx.cpu().numpy(), _ref_idx(a, k, False))
+
+
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_large_k_from_stream_counts(gpu, largest):
+    """k > n / 1024 on the window path with 16-byte aligned keys: the tile counts
+    come from the streaming pass's per-row words (#beyond the window, #on each
+    edge) plus the candidates' rows (k_main<3/4>, k_topk_cands), not from a
+    second read of the input.  Families put the k-th on a window edge (narrow,
+    few distinct: heavy ties at lo / hi), strictly inside it (uniform), or
+    outside it (spike at the median: window miss, counted from the input); the
+    ragged tail past k_main's full tiles is counted from the input."""
+    import torch
+    n = (1 << 23) + 4099
+    rng = np.random.default_rng(31 + largest)
+    uni = rng.integers(-2 ** 31, 2 ** 31, size=n, dtype=np.int64).astype(np.int32)
+    narrow = rng.integers(-300, 300, size=n).astype(np.int32)
+    few = rng.integers(-3, 4, size=n).astype(np.int32)
+    spike = uni.copy()
+    spike[rng.random(n) < 0.4] = -99
+    for name, a in (("uniform", uni), ("narrow", narrow), ("few", few), ("spike", spike)):
+        d = torch.from_numpy(a).cuda()
+        for k in (n // 1024 + 1, n // 3, n // 2, n - 5):
+            vals, idx = _run(gpu, d, n, k, largest)
+            want = _ref_idx(a, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k}")
+            np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{name} k={k}")
+            assert gpu.stats()["error"] == 0
