@@ -181,6 +181,58 @@ struct CoherentBuf {
     }
 };
 
+// k_head's gather of the full 1024-key sample chunks: the first digit of a
+// fresh selection has one histogram (both window targets share the empty
+// prefix) and no prefix test, so a key costs a shift and one LDS atomic; the
+// chunk is written through as 16-byte stores (per-key 4-byte atomic stores and
+// bounds tests made the gather ~8 us of VALU issue in 64 CUs).  Chunk c of the
+// sample = keys[c * stride, + SAMPLE_CHUNK); lane l holds 16-byte words l, l+64,
+// l+128, l+192 of it.  Returns false (nothing done) unless every chunk is full
+// and 16-byte aligned; the caller then uses gather_chunks.
+template <int BLOCK>
+__device__ __forceinline__ bool gather_head_fast(const int32_t *__restrict__ keys, u64 stride, uint32_t *sample,
+                                                 u64 s, uint32_t (*lh)[NBINS], const HistPlan &plan) {
+    static_assert(SAMPLE_CK == 16, "four 16-byte words per lane and chunk");
+    // (selects, not plan.x[t]: a runtime index made the plan a private array
+    // that the compiler moved into 44 KiB of LDS)
+    const bool one = plan.h[0] != plan.h[1];  // exactly one histogram
+    const bool t1 = !plan.h[0];
+    if (s % SAMPLE_CHUNK != 0 || (reinterpret_cast<uintptr_t>(keys) & 15u) != 0 || stride % 4 != 0 || !one ||
+        (t1 ? plan.done[1] : plan.done[0]) != 0 || plan.base != 0u)
+        return false;
+    const uint32_t sh = t1 ? plan.shift[1] : plan.shift[0], mask = t1 ? plan.mask[1] : plan.mask[0];
+    uint32_t *h = t1 ? lh[1] : lh[0];
+    const __amdgpu_buffer_rsrc_t out =
+        __builtin_amdgcn_make_buffer_rsrc(sample, (short)0, (int)(s * 4), 0x00020000);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const u64 nchunks = s / SAMPLE_CHUNK;
+    const u64 gw = ((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (BLOCK / WAVE);
+    for (u64 c = gw; c < nchunks; c += nw) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
+        uint4 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            q[r].x ^= 0x80000000u;
+            q[r].y ^= 0x80000000u;
+            q[r].z ^= 0x80000000u;
+            q[r].w ^= 0x80000000u;
+            u32x4 v = {q[r].x, q[r].y, q[r].z, q[r].w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, out, (int)((c * SAMPLE_CHUNK + 4 * (r * WAVE + lane)) * 4), 0,
+                                                   16 /* sc1: written through */);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            atomicAdd(&h[(q[r].x >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].y >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].z >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].w >> sh) & mask], 1u);
+        }
+    }
+    return true;
+}
+
 __device__ __forceinline__ uint32_t active_wgs(u64 count, u64 per_wg) {
     const u64 want = (count + per_wg - 1) / per_wg;
     return (uint32_t)(want < (u64)gridDim.x ? want : (u64)gridDim.x);
@@ -202,9 +254,17 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     advance<DENSE_BLK>(ss, a, scratch);
     bool share;
     HistPlan plan = make_plan(ss, &share);
-    gather_chunks<DENSE_BLK, true, true>(keys, n_keys, stride, sample, s, lh, plan);
+    if (!gather_head_fast<DENSE_BLK>(keys, stride, sample, s, lh, plan))  // block-uniform
+        gather_chunks<DENSE_BLK, true, true>(keys, n_keys, stride, sample, s, lh, plan);
+#ifdef KTH_HEAD_DIAG  // diagnostic build: gather / flush / drain times (slots 4-6 are free on an early window)
+    KTH_STAMP(a, 4);
+#endif
     hist_flush<DENSE_BLK>(lh, plan, x.slots);
     KTH_STAMP(a, 1);
+#ifdef KTH_HEAD_DIAG
+    wait_mem();
+    KTH_STAMP(a, 6);
+#endif
     const EarlyWindow ew{a.r_lo, a.r_hi, x.slack64};
     bool ok = true;
     for (int L = 0;; ++L) {
