@@ -340,8 +340,8 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
 //     and the sample phase's slots (x.zero2) are cleared here too: no barrier
 //     after the last level.
 constexpr int FIN_LDS_KEYS = 32768;  // LDS-resident keys per workgroup (128 KiB of dynamic LDS)
-constexpr int FIN_UNROLL = 4;        // 16-B loads in flight per thread (1024-thread workgroups: <= 128 VGPRs)
 constexpr uint32_t FIN_D0 = 9;  // [257, 512] bins used: ~12-25 K keys a bin from 6.3 M candidates
+constexpr int FIN_UNROLL = 4;        // 16-B loads in flight per thread (1024-thread workgroups: <= 128 VGPRs)
 
 __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPlan &plan, const uint4 &x, bool xr,
                                             uint32_t valid4) {
@@ -368,8 +368,9 @@ constexpr uint32_t TAIL_STAGE = 2 * NBINS;  // keys a workgroup stages in LDS (t
 
 __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, uint4 *res, u64 nk, bool xr,
                             uint32_t (*lh)[NBINS], u64 *scratch) {
-    __shared__ uint32_t s_n, s_last, s_total;
-    __shared__ u64 s_off;
+    __shared__ uint32_t s_n, s_last, s_total, s_ln;
+    __shared__ uint32_t s_list[WAVE];
+    __shared__ u64 s_off, s_c;
     const uint32_t X = xr ? 0x80000000u : 0u;
     const uint32_t W = ss.W, base = ss.base, done = ss.t[0].done, prefix = ss.t[0].prefix;
     const uint32_t psh = W - done;  // done >= 1: a level was picked
@@ -459,6 +460,7 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
     // with a key of another bin of the entry digit, which matches no later
     // prefix either
     const uint32_t nq = (total + 3) / 4;
+    const uint32_t pad = base + ((prefix ^ 1u) << psh);  // a key of another bin of the entry digit
     {
         constexpr int TU = FIN_LDS_KEYS / 4 / DENSE_BLK;
         static_assert(TU % FIN_UNROLL == 0, "tail loads in FIN_UNROLL batches");
@@ -475,7 +477,6 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
             for (int u = 0; u < FIN_UNROLL; ++u) {
                 const uint32_t v = (u0 + u) * DENSE_BLK + threadIdx.x;
                 if (v == total / 4 && (total & 3u)) {
-                    const uint32_t pad = base + ((prefix ^ 1u) << psh);
                     if ((total & 3u) <= 1) q[u].y = pad;
                     if ((total & 3u) <= 2) q[u].z = pad;
                     q[u].w = pad;
@@ -509,10 +510,55 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
         u64 h0[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) h0[j] = lh[0][threadIdx.x * PER + j];
-        pick_state<DENSE_BLK, PER>(ss, h0, h0, true, scratch, nullptr);
+        pick_state<DENSE_BLK, PER>(ss, h0, h0, true, scratch, nullptr, &s_c);
 #ifdef KTH_STAMPS_BUILD
         if (it < 2) KTH_STAMP(a, 1 + it);  // diagnostic only: the finisher overwrites its own early stamps
 #endif
+        // <= 64 keys left in the picked bin (uniform keys: ~8): list them and
+        // rank them in one wave instead of another histogram level
+        if ((ss.mode == MODE_CAND || ss.mode == MODE_FULL) && s_c <= (u64)WAVE) {  // block-uniform
+            const uint32_t dl = ss.t[0].done, pl = ss.t[0].prefix, msl = W - dl;  // 1 <= dl < W
+            if (threadIdx.x == 0) s_ln = 0;
+            __syncthreads();
+            auto put = [&](uint32_t key) {  // wave-convergent
+                const bool m = ((key - base) >> msl) == pl;
+                const u64 b = __ballot(m);
+                if (b == 0) return;
+                uint32_t at = 0;
+                if (lane == 0) at = atomicAdd(&s_ln, (uint32_t)__popcll(b));
+                at = __shfl(at, 0, WAVE);
+                const uint32_t i = at + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                if (m && i < (uint32_t)WAVE) s_list[i] = key;
+            };
+            for (uint32_t v0 = 0; v0 < nq; v0 += DENSE_BLK) {
+                const uint32_t v = v0 + threadIdx.x;
+                const uint4 q = v < nq ? res[v] : make_uint4(pad, pad, pad, pad);
+                put(q.x);
+                put(q.y);
+                put(q.z);
+                put(q.w);
+            }
+            __syncthreads();
+            if (threadIdx.x < WAVE) {
+                const uint32_t ln = s_ln < (uint32_t)WAVE ? s_ln : (uint32_t)WAVE;
+                const uint32_t mine = (uint32_t)lane < ln ? s_list[lane] : 0u;
+                uint32_t lt = 0, le = 0;
+                for (uint32_t j = 0; j < ln; ++j) {
+                    const uint32_t o = s_list[j];
+                    lt += o < mine ? 1u : 0u;
+                    le += o <= mine ? 1u : 0u;
+                }
+                const u64 kk = ss.t[0].k;
+                const bool hit = (uint32_t)lane < ln && (u64)lt < kk && kk <= (u64)le;
+                if (hit) ss.answer = mine;  // equal keys write the same value
+                if (__ballot(hit) == 0 && lane == 0) ss.error = 33;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) ss.mode = MODE_DONE;
+            __syncthreads();
+            break;
+        }
     }
     KTH_STAMP(a, 3);
     return true;
@@ -561,6 +607,17 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         if (resident) {
             const uint32_t nv = (uint32_t)((nk + 3) / 4);
             if (L == 0) {  // HBM -> registers -> histogram + LDS
+                // the domain's first digit: one target, no prefix yet, so a full
+                // vector's keys cost a subtract, a shift and an LDS atomic each
+                // (hist_add's generic two-target path was ~2x the VALU issue)
+                const bool one = plan.h[0] && !plan.h[1] && plan.done[0] == 0;
+                const uint32_t X = xr ? 0x80000000u : 0u, bs = plan.base, sh = plan.shift[0], mk = plan.mask[0];
+                auto add4 = [&](const uint4 &q) {
+                    atomicAdd(&lh[0][(((q.x ^ X) - bs) >> sh) & mk], 1u);
+                    atomicAdd(&lh[0][(((q.y ^ X) - bs) >> sh) & mk], 1u);
+                    atomicAdd(&lh[0][(((q.z ^ X) - bs) >> sh) & mk], 1u);
+                    atomicAdd(&lh[0][(((q.w ^ X) - bs) >> sh) & mk], 1u);
+                };
                 if (aligned) {
                     const uint4 *src = reinterpret_cast<const uint4 *>(dom + b0);
                     for (uint32_t v0 = 0; v0 < nv; v0 += FIN_UNROLL * DENSE_BLK) {
@@ -575,9 +632,11 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
                             const uint32_t v = v0 + u * DENSE_BLK + threadIdx.x;
                             if (v < nv) {
                                 const u64 e = 4ull * v;
-                                const uint32_t valid4 = nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u;
                                 res[v] = q[u];
-                                finish_keys(lh, plan, q[u], xr, valid4);
+                                if (one && nk - e >= 4)
+                                    add4(q[u]);
+                                else
+                                    finish_keys(lh, plan, q[u], xr, nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u);
                             }
                         }
                     }
