@@ -200,6 +200,11 @@ double kth_window_z(void);
  * max(2^20, n_local / 32); more candidates than this on a rank set its
  * overflow count and the selection takes the exact fallback levels. */
 int64_t kth_dist_cand_capacity(int64_t n_local);
+/* Early-window slack of the sample phase, in 1/64ths: after each sample digit,
+ * the window stops at the picked bins' edges when those hold at most
+ * slack/64 times the sample keys the exact window would (96 = 1.5; the
+ * KTH_HEAD_SLACK environment variable changes a new ctx's value, 0 = off). */
+int kth_window_slack64(void);
 
 /* --- sharded selection, one process driving several GPUs ---------------------
  * Replaces TODO-kth-problem-cgm.c:81-278 (block partition + Scatterv, the

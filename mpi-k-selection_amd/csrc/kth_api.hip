@@ -116,6 +116,7 @@ struct kth_ctx {
     bool dirty = false;  // a launch sequence was cut short: re-zero the slots
     bool dist_zero = false;  // sharded: the bound slots still need clearing
     bool dist_open = false;  // sharded: begun, kth_dist_result not yet enqueued
+    bool dist_coop_window = false;  // sharded: the window came from k_head (state carried, no pick left)
     // KTH_STAMPS=1 diagnostics: per-launch [WG][8] wall-clock stamps, dumped after each select
     u64 *stamps = nullptr;
     int stamp_next = 0;
@@ -1003,6 +1004,8 @@ double kth_window_z(void) { return window_z(); }
 
 int64_t kth_dist_cand_capacity(int64_t n_local) { return (int64_t)cand_capacity(std::max<int64_t>(n_local, 1)); }
 
+int kth_window_slack64(void) { return (int)(HEAD_SLACK * 64); }
+
 int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;
     KTH_TRY(set_device(c));
@@ -1046,6 +1049,26 @@ int kth_dist_window(kth_ctx *c, const uint32_t *d_sample, int64_t s_total) {
     }
     u64 r_lo, r_hi;
     window_ranks(c->dist_n, c->dist_k, s_total, &r_lo, &r_hi);
+    if (c->coop && s_total % 64 == 0 && s_total < (1ll << 29)) {
+        // one cooperative launch over the gathered sample (k_head without its
+        // gather): the digits behind grid barriers, the early window; the state
+        // is left resolved in st[0] for kth_dist_scan (ADV_CARRY).  Its slots
+        // are cleared by kth_dist_result's k_result.
+        StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, nullptr, nullptr);
+        a.init_n = (u64)c->dist_n;
+        a.init_k = (u64)c->dist_k;
+        a.init_s = (u64)s_total;
+        a.r_lo = r_lo;
+        a.r_hi = r_hi;
+        kth::CoopArgs x = coop_args(c, HSLOT_OFF, nullptr, nullptr);
+        x.sample_ready = 1;
+        const int grid = (int)std::min<int64_t>(64, std::max<int64_t>(1, s_total / (16 * 1024)));
+        kth::k_head<<<grid, kth::DENSE_BLK, 0, c->stream>>>(a, x, nullptr, 0, 0, const_cast<uint32_t *>(d_sample),
+                                                           (u64)s_total);
+        c->dist_coop_window = true;
+        return launch_check();
+    }
+    c->dist_coop_window = false;
     StepArgs a = step(c, kth::ADV_INIT_SAMPLE, -1, 0, nullptr, islot(c, 1), islot(c, 2));
     a.init_n = (u64)c->dist_n;
     a.init_k = (u64)c->dist_k;
@@ -1071,7 +1094,8 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     if (!c || !d_keys || n_local < 0 || !c->uslots) return KTH_EINVAL;
     KTH_TRY(set_device(c));
     KTH_TRY(reserve_cand(c, std::max<int64_t>(n_local, 1)));
-    StepArgs a = step(c, kth::ADV_PICK, 0, 1, islot(c, 0), c->uslots, nullptr);
+    StepArgs a = c->dist_coop_window ? step(c, kth::ADV_CARRY, 0, 1, nullptr, c->uslots, nullptr)
+                                     : step(c, kth::ADV_PICK, 0, 1, islot(c, 0), c->uslots, nullptr);
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
@@ -1106,7 +1130,8 @@ int kth_dist_result(kth_ctx *c, int32_t *d_out) {
     const int in = KTH_DIST_LEVELS % 3;  // slot written by the last level
     const int st_in = (KTH_DIST_LEVELS - 1) % 2;
     StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)in * KTH_STATS_WORDS, nullptr, nullptr);
-    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots, ISLOT_WORDS);
+    // (the islots and, right after them, k_head's slots of a cooperative window)
+    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots, ISLOT_WORDS + HSLOT_WORDS);
     c->last_state = 1 - st_in;
     c->dist_level_next = -1;
     c->dist_open = false;

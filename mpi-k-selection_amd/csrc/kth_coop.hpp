@@ -42,6 +42,7 @@ struct CoopArgs {
     u64 *zero2;        // k_finish: a second region to clear (the sample phase's slots)
     u64 zero2_words;
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
+    uint32_t sample_ready;  // k_head: the sample (order keys) is already in `sample` (sharded window)
 };
 
 // This wave's outstanding global accesses (atomics, write-through stores) are
@@ -238,7 +239,9 @@ __device__ __forceinline__ uint32_t active_wgs(u64 count, u64 per_wg) {
     return (uint32_t)(want < (u64)gridDim.x ? want : (u64)gridDim.x);
 }
 
-// Sample phase: init (ADV_INIT_SAMPLE: a.init_*, a.r_lo / r_hi) -> gather +
+// Sample phase (x.sample_ready: the sharded window over an all-gathered
+// sample -- no gather, the first digit read from `sample`): init
+// (ADV_INIT_SAMPLE: a.init_*, a.r_lo / r_hi) -> gather +
 // first digit -> up to two more sample digits, each behind a grid barrier.
 // Workgroup 0 publishes the state in a.st_out: MODE_MAIN with the window, or
 // MODE_DONE with an error.  Replaces k_gather<true> + two k_level launches.
@@ -254,7 +257,32 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     advance<DENSE_BLK>(ss, a, scratch);
     bool share;
     HistPlan plan = make_plan(ss, &share);
-    if (!gather_head_fast<DENSE_BLK>(keys, stride, sample, s, lh, plan))  // block-uniform
+    // a digit of the sample (written through by every workgroup's gather, or
+    // already there) in 16-byte sc1 loads, HEAD_UNROLL per thread in flight;
+    // s is a multiple of 64
+    auto hist_sample = [&]() {
+        const CoherentBuf sb(sample, (uint32_t)(s * 4));
+        const uint32_t nv = (uint32_t)(s / 4), per = DENSE_BLK * HEAD_UNROLL;
+        for (uint32_t v0 = blockIdx.x * per; v0 < nv; v0 += gridDim.x * per) {
+            uint4 q[HEAD_UNROLL];
+#pragma unroll
+            for (int u = 0; u < HEAD_UNROLL; ++u) {
+                const uint32_t v = v0 + u * DENSE_BLK + threadIdx.x;
+                q[u] = sb.load16(v < nv ? v * 16u : 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < HEAD_UNROLL; ++u) {
+                const bool in = v0 + u * DENSE_BLK + threadIdx.x < nv;
+                hist_add<DENSE_BLK>(lh, plan, q[u].x, in);
+                hist_add<DENSE_BLK>(lh, plan, q[u].y, in);
+                hist_add<DENSE_BLK>(lh, plan, q[u].z, in);
+                hist_add<DENSE_BLK>(lh, plan, q[u].w, in);
+            }
+        }
+    };
+    if (x.sample_ready)  // block-uniform
+        hist_sample();
+    else if (!gather_head_fast<DENSE_BLK>(keys, stride, sample, s, lh, plan))
         gather_chunks<DENSE_BLK, true, true>(keys, n_keys, stride, sample, s, lh, plan);
 #ifdef KTH_HEAD_DIAG  // diagnostic build: gather / flush / drain times (slots 4-6 are free on an early window)
     KTH_STAMP(a, 4);
@@ -279,26 +307,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
         for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK)
             reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        // the sample (written through by every workgroup's gather) in 16-byte
-        // sc1 loads, HEAD_UNROLL per thread in flight; s is a multiple of 64
-        const CoherentBuf sb(sample, (uint32_t)(s * 4));
-        const uint32_t nv = (uint32_t)(s / 4), per = DENSE_BLK * HEAD_UNROLL;
-        for (uint32_t v0 = blockIdx.x * per; v0 < nv; v0 += gridDim.x * per) {
-            uint4 q[HEAD_UNROLL];
-#pragma unroll
-            for (int u = 0; u < HEAD_UNROLL; ++u) {
-                const uint32_t v = v0 + u * DENSE_BLK + threadIdx.x;
-                q[u] = sb.load16(v < nv ? v * 16u : 0u);
-            }
-#pragma unroll
-            for (int u = 0; u < HEAD_UNROLL; ++u) {
-                const bool in = v0 + u * DENSE_BLK + threadIdx.x < nv;
-                hist_add<DENSE_BLK>(lh, plan, q[u].x, in);
-                hist_add<DENSE_BLK>(lh, plan, q[u].y, in);
-                hist_add<DENSE_BLK>(lh, plan, q[u].z, in);
-                hist_add<DENSE_BLK>(lh, plan, q[u].w, in);
-            }
-        }
+        hist_sample();
         hist_flush<DENSE_BLK>(lh, plan, x.slots + (size_t)(L + 1) * STATS_WORDS);
         if (L == 0) KTH_STAMP(a, 4);
     }

@@ -527,7 +527,27 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
         for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < a.zero_words; i += (u64)gridDim.x * DENSE_BLK)
             a.stats_zero[i] = 0;
     }
-    gather_chunks<DENSE_BLK, FUSE>(keys, n_keys, stride, sample, s, lh, plan);
+    // (sharded sample, full aligned chunks: a chunk is copied as 16-byte words
+    // in the layout gather_chunks writes -- the per-key path took ~8 us)
+    const bool vec = !FUSE && s % SAMPLE_CHUNK == 0 && (reinterpret_cast<uintptr_t>(keys) & 15u) == 0 &&
+                     stride % 4 == 0 && SAMPLE_CK == 16;
+    if (vec) {
+        const int lane = threadIdx.x & (WAVE - 1);
+        const u64 nch = s / SAMPLE_CHUNK;
+        for (u64 c = ((u64)blockIdx.x * DENSE_BLK + threadIdx.x) / WAVE; c < nch; c += (u64)gridDim.x * (DENSE_BLK / WAVE)) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
+            uint4 *dst = reinterpret_cast<uint4 *>(sample + c * SAMPLE_CHUNK);
+            uint4 q[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                dst[r * WAVE + lane] = make_uint4(q[r].x ^ 0x80000000u, q[r].y ^ 0x80000000u, q[r].z ^ 0x80000000u,
+                                                  q[r].w ^ 0x80000000u);
+        }
+    } else {
+        gather_chunks<DENSE_BLK, FUSE>(keys, n_keys, stride, sample, s, lh, plan);
+    }
     KTH_STAMP(a, 3);
     if (FUSE) hist_flush<DENSE_BLK>(lh, plan, a.stats_acc);
     KTH_STAMP(a, 5);

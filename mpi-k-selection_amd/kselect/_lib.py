@@ -106,6 +106,7 @@ PROTOS = {
     "kth_sample_chunk": (ctypes.c_int, []),
     "kth_window_z": (ctypes.c_double, []),
     "kth_dist_cand_capacity": (ctypes.c_int64, [ctypes.c_int64]),
+    "kth_window_slack64": (ctypes.c_int, []),
     "kth_sharded_create": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.POINTER(c_vp)]),
     "kth_sharded_destroy": (ctypes.c_int, [c_vp]),
     "kth_sharded_select_i32": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_i32p]),

@@ -23,6 +23,8 @@ C_LT, C_EQLO, C_EQHI, C_IN, C_OVF = range(5)
 MAIN, CAND, FULL, DONE = "main", "cand", "full", "done"
 WINDOW_Z = float(LIB.kth_window_z())
 SAMPLE_CHUNK = int(LIB.kth_sample_chunk())
+WINDOW_SLACK64 = int(LIB.kth_window_slack64())
+SAMPLE_DIGITS = (11, 11, 10)  # k_head's digits of a 32-bit sample key
 
 
 def sample_size(n_local):
@@ -91,11 +93,32 @@ class CpuBackend:
         out.numpy()[:] = keys.view(np.int32)
 
     def window(self, sample_all, s_total):
+        """k_head over the gathered sample (kth_dist_window): the window ranks'
+        keys digit by digit; after each digit the window may stop at the picked
+        bins' edges when those hold at most WINDOW_SLACK64/64 times the sample
+        keys of the exact window (kth_kernels.hip early_window)."""
         r_lo, r_hi = window_ranks(self.n, self.k, s_total)
         srt = np.sort(sample_all.numpy().view(np.uint32))
-        self.lo = int(srt[r_lo - 1]) if 1 <= r_lo <= s_total else 0
-        self.hi = int(srt[r_hi - 1]) if 1 <= r_hi <= s_total else 0xFFFFFFFF
+        a0, a1 = 1 <= r_lo <= s_total, 1 <= r_hi <= s_total
         self.mode = MAIN
+        if (a0 or a1) and WINDOW_SLACK64 and s_total % 64 == 0:
+            want = (r_hi if a1 else s_total) - (r_lo if a0 else 1) + 1
+            done = 0
+            for d in SAMPLE_DIGITS[:-1]:  # the last digit resolves the exact keys
+                done += d
+                sh = np.uint32(32 - done)
+                pre = srt >> sh
+                p0 = int(srt[r_lo - 1] >> sh) if a0 else 0
+                p1 = int(srt[r_hi - 1] >> sh) if a1 else 0
+                below0 = int(np.searchsorted(pre, np.uint32(p0), side="left")) if a0 else 0
+                upto1 = int(np.searchsorted(pre, np.uint32(p1), side="right")) if a1 else s_total
+                if upto1 >= below0 and (upto1 - below0) * 64 <= want * WINDOW_SLACK64:
+                    w = 32 - done
+                    self.lo = p0 << w if a0 else 0
+                    self.hi = ((p1 << w) | ((1 << w) - 1)) if a1 else 0xFFFFFFFF
+                    return
+        self.lo = int(srt[r_lo - 1]) if a0 else 0
+        self.hi = int(srt[r_hi - 1]) if a1 else 0xFFFFFFFF
 
     def scan(self, shard, n_local):
         u = shard.numpy()[:n_local].view(np.uint32) ^ np.uint32(0x80000000)

@@ -473,7 +473,7 @@ def test_dist_world1_nccl(gpu):
                 srt = np.sort(keys.cpu().numpy())
                 for k in (1, n // 2, n):
                     got = int(ds.select(keys, n, n, k).item())
-                    assert got == srt[k - 1], (fam, k, type(ds.comm).__name__)
+                    assert got == srt[k - 1], (fam, k, type(ds.comm).__name__, b.sel.stats())
             ds.close()
     finally:
         dist.destroy_process_group()
