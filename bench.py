@@ -518,6 +518,20 @@ def main():
     barrier()
     n_sel, main_ms, total_ms = sel.take_timing()
     elapsed = t1 - t0
+    # the same steps once more with no HIP events on the stream (diagnostic:
+    # timing events switch the queue to timestamped dispatches, ~10 us a select)
+    sel.enable_timing(False)
+    torch.cuda.synchronize()
+    barrier()
+    t2 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    elapsed_ne = time.perf_counter() - t2
+    if world > 1:
+        t = torch.tensor([elapsed_ne], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed_ne = float(t.item())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -583,6 +597,7 @@ def main():
         "verified": bool(verified),
         "answer": v,
         "whole_select_ms_events": total_ms / max(1, n_sel) if not sharded else None,
+        "ms_per_step_no_events": elapsed_ne * 1e3 / args.steps,
     }
     if stats:
         res["path"] = {1: "lds", 2: "radix", 3: "window", 4: "window_fallback"}.get(stats["path"], "?")
