@@ -130,6 +130,31 @@ def test_window_path_fuzz(gpu, kind):
             assert gpu.select(d, k) == want, (kind, n, k, gpu.stats())
 
 
+@pytest.mark.parametrize("copies,spread", [(6000, 1), (20000, 1), (9000, 40), (40000, 3)])
+def test_finish_tail_clustered_block(gpu, copies, spread):
+    """k_finish's tail at 2^28 keys (~1.3 M candidates, ~5 K per workgroup
+    slice): a contiguous block of near-duplicate keys at the median lands in a
+    few slices, so a slice can hold more of the picked bin's keys than its LDS
+    stage (the second append scan), or the bin more than one workgroup's LDS
+    (40000: no tail, grid levels); spread > 1 leaves several values in the last
+    bin (the one-wave list rank).  Checked by the exact rank certificate
+    #(< v) < k <= #(<= v) on the device."""
+    import torch
+    n = 1 << 28
+    d = _dev_keys(gpu, n, "uniform_full")
+    med = gpu.select(d, n // 2)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(copies + spread)
+    start = (n // 3 + copies * 7919) % (n - copies)
+    d[start:start + copies] = med + torch.randint(0, spread, (copies,), device="cuda", dtype=torch.int32,
+                                                  generator=g)
+    torch.cuda.synchronize()
+    for k in (n // 2 - copies // 3, n // 2, n // 2 + 1, n // 2 + copies // 2):
+        v = gpu.select(d, k)
+        lt, le = int((d < v).sum()), int((d <= v).sum())
+        assert lt < k <= le, (copies, spread, k, v, lt, le, gpu.stats())
+
+
 def test_unaligned_device_pointer(gpu):
     """Shards start anywhere: 4-byte but not 16-byte aligned inputs."""
     import torch
