@@ -649,8 +649,9 @@ __device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
 }
 
-// k_main<3/4>'s per-row tallies of one tile (this lane): #beyond (#<lo for
-// RW 3, #>hi for 4) of row u in r[u] (one add-with-carry a key).  Counted
+// k_main<3/4>'s per-row tallies of one tile (this lane): RW 4: #>hi of row u
+// in r[u] (one add-with-carry a key); RW 3: the lane's running #<lo (clt)
+// after row u, differenced per row afterwards (no extra work per key).  Counted
 // where the compares are made (a second set of compares elsewhere kept compare
 // masks live in SGPRs and made the loop spill them).
 struct RowAcc {
@@ -671,8 +672,10 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
         clt += (ok & (x < slo)) ? 1u : 0u;
         ceqlo += (ok & (x == slo)) ? 1u : 0u;
         ceqhi += (ok & (x == shi)) ? 1u : 0u;
-        if constexpr (RW != 0) {
-            ra->r[j / 4] += (RW == 3 ? x < slo : x > shi) ? 1u : 0u;
+        if constexpr (RW == 3) {  // #<lo is clt's own count: a snapshot after each row's 4 keys
+            if ((j & 3) == 3) ra->r[j / 4] = clt;
+        } else if constexpr (RW == 4) {
+            ra->r[j / 4] += x > shi ? 1u : 0u;
         }
         st.slot((uint32_t)x ^ 0x80000000u, ok & (x > slo) & (x < shi), row0 == ~0u ? ~0u : row0 + (uint32_t)(j / 4));
     }
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     // loads wait for the store: +70 us a pass); pend_at = word index (~0: none).
     u64 pend_at = ~0ull;
     uint32_t pend_word = 0;
-    auto flag_tile = [&](const uint4 (&x)[U], u64 t, const RowAcc &ra, uint32_t e0) {
+    auto flag_tile = [&](const uint4 (&x)[U], u64 t, RowAcc &ra, uint32_t e0, uint32_t c0) {
         if constexpr (TF == 1 || TF == 2) {
             // bit u of the wave's byte: some key of row u (the tile's u-th run of
             // 4 * BLK keys) in this wave's part is <= hi (TF 1) / >= lo (TF 2)
@@ -798,6 +801,11 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             // wave-tile with a key on a window edge (uniform keys: never) is
             // marked TK_RECOUNT instead: the count pass reads those rows (per-row
             // edge tallies here made the loop spill SGPRs too).
+            if constexpr (TF == 3) {  // running #<lo snapshots -> per-row counts
+#pragma unroll
+                for (int u = U - 1; u > 0; --u) ra.r[u] -= ra.r[u - 1];
+                ra.r[0] -= c0;
+            }
             // rows 0-3 / 4-7 into the 8-bit fields of b0 / b1 (a lane's row count <= 4)
             uint32_t b0 = ra.r[0] | ra.r[1] << 8 | ra.r[2] << 16 | ra.r[3] << 24;
             uint32_t b1 = ra.r[4] | ra.r[5] << 8 | ra.r[6] << 16 | ra.r[7] << 24;
@@ -833,12 +841,12 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
-        const uint32_t e0 = ceqlo + ceqhi;
+        const uint32_t e0 = ceqlo + ceqhi, c0 = clt;
         load_tile(x, t);
         if constexpr (TF >= 3)
             if (pend_at != ~0ull) tflags[pend_at] = pend_word;  // the previous tile's words (lanes 0..U-1)
         scan_tile(x, t, ra);
-        flag_tile(x, t, ra, e0);
+        flag_tile(x, t, ra, e0, c0);
     }
     if constexpr (TF >= 3)
         if (pend_at != ~0ull) tflags[pend_at] = pend_word;
