@@ -417,8 +417,8 @@ def topk_main(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--log2n", type=int, default=30, help="keys per GPU = 2^log2n")
     ap.add_argument("--family", default="uniform_half")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
