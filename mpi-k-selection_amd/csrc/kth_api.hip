@@ -925,11 +925,12 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     // count and write passes: one wave per 64 tiles
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
-    if (tf >= 3) {
-        kth::k_topk_count<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
-                                                                          tcnt, tflags, head, nfull, sel_st, ncov);
+    if (tf >= 3) {  // candidates' share first (atomics into zeroed counts), then the rows' words
+        HIP_TRY(hipMemsetAsync(tcnt, 0, ntiles * 4, c->stream));
         kth::k_topk_cands<<<c->num_cu * 8, kth::TK_BLOCK, 0, c->stream>>>(
             c->cand, c->cand_rows, cand_count(c), c->cand_cap / 4, c->d_status, flip, tcnt, tflags, sel_st);
+        kth::k_topk_count<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+                                                                          tcnt, tflags, head, nfull, sel_st, ncov);
     } else if (aligned) {
         kth::k_topk_count<true, false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                            tcnt, tflags, head, nfull, sel_st, 0);

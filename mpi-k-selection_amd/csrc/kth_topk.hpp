@@ -71,7 +71,7 @@ __device__ __forceinline__ bool tk_meta_ok(const uint32_t *tflags, const int32_t
 }
 
 // a tile count word: #better | #equal << 16, plus TK_RECOUNT (bit 31) on a
-// META tile counted from the input (k_topk_cands then leaves it alone)
+// META tile counted from the input (its candidates' share, added before, is overwritten)
 __device__ __forceinline__ uint32_t tk_better_of(uint32_t c) { return c & 0xFFFFu; }
 __device__ __forceinline__ uint32_t tk_equal_of(uint32_t c) { return (c >> 16) & 0x7FFFu; }
 
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
         if (act && meta_ok && tl < ncov) {
             const uint4 w = reinterpret_cast<const uint4 *>(fw)[tl];
             if (((w.x | w.y | w.z | w.w) & TK_RECOUNT) == 0u) {
-                tcnt[tl] = w.x + w.y + w.z + w.w;  // <= 1024
+                tcnt[tl] += w.x + w.y + w.z + w.w;  // k_topk_cands ran first: add to the candidates' share
                 act = false;
             }
         }
@@ -159,9 +159,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
     }
 }
 
-// Pass 1b (META): the candidates' share of their rows' counts (one atomic per
-// candidate that is better than or equal to v; rows past ncov were counted
-// from the input and carry row ~0u).
+// Pass 0 (META, before k_topk_count, into zeroed counts): the candidates'
+// share of their rows' counts, one atomic per candidate better than or equal
+// to v (no read: a row k_topk_count then counts from the input is simply
+// overwritten there; rows past ncov carry row ~0u).
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restrict__ cand,
                                                          const uint32_t *__restrict__ rows,
                                                          const u64 *__restrict__ cand_count, u64 cap,
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restr
     const u64 m = min(*cand_count, cap);
     for (u64 i = (u64)blockIdx.x * TK_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * TK_BLOCK) {
         const uint32_t r = rows[i];
-        if (r == ~0u || (tcnt[r] & TK_RECOUNT)) continue;  // outside k_main's rows / counted from the input
+        if (r == ~0u) continue;  // outside k_main's rows (counted from the input)
         const uint32_t u = cand[i];
         if (tk_better(u, uv, flip))
             atomicAdd(&tcnt[r], 1u);
