@@ -313,13 +313,9 @@ def rows_main(args):
     keys_total = R * C * world
     value = keys_total / (elapsed / args.steps) / 1e9
     achieved = 4.0 * R * C / (kern_ms * 1e-3) / 1e9
-    rows_traffic = None  # PMC HBM bytes per launch (tools/gpu_profiles.sh), for this exact workload
-    tpath = os.path.join(REPO, "profiles", f"pmc_traffic_rows_{args.rows_dtype}.json")
-    if os.path.exists(tpath) and not args.topk and (R, C, k) == (65536, 4096, 64):
-        try:
-            rows_traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            rows_traffic = None
+    rows_traffic, rows_note = None, "no PMC measurement for this workload"
+    if not args.topk and (R, C, k) == (65536, 4096, 64):
+        rows_traffic, rows_note = pmc_traffic(f"pmc_traffic_rows_{args.rows_dtype}.json", None, None)
     res = {
         "metric": ("Gkeys/s batched top-k (largest) per row" if args.topk else "Gkeys/s batched k-th per row")
                   + " (65536 x 4096, BASELINE config 5)",
@@ -332,7 +328,7 @@ def rows_main(args):
                    "rows": R, "cols": C, "k": k, "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "kth::k_rows_reg" if C <= 4096 else "kth::k_rows",
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": rows_traffic,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": rows_traffic, "traffic_source": rows_note,
                      "algorithmic_bytes_per_launch": 4 * R * C, "avg_launch_ms": kern_ms},
         "verified": verified,
     }
@@ -341,6 +337,25 @@ def rows_main(args):
     if world > 1:
         dist.destroy_process_group()
     return 0 if verified else 1
+
+
+def pmc_traffic(name, log2n, family):
+    """HBM bytes per launch of the dominant kernel from profiles/<name> (two
+    rocprofv3 --pmc passes, tools/pmc_traffic.py), used only when it was
+    measured on the libkth.so build loaded now (kth_build_id) and on this
+    workload; otherwise (None, reason)."""
+    import kselect
+    path = os.path.join(REPO, "profiles", name)
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None, f"profiles/{name} missing or unreadable"
+    here = kselect.LIB.kth_build_id().decode()
+    if tj.get("build_id") != here:
+        return None, f"profiles/{name} was measured on libkth build {tj.get('build_id')}, loaded build is {here}"
+    if log2n is not None and (tj.get("log2n"), tj.get("family")) != (log2n, family):
+        return None, f"profiles/{name} is for 2^{tj.get('log2n')} {tj.get('family')}, not this workload"
+    return tj.get("hbm_bytes_per_launch"), f"profiles/{name} (PMC FETCH_SIZE/WRITE_SIZE, build {here})"
 
 
 def topk_main(args):
@@ -551,15 +566,7 @@ def main():
     value = n_total / (elapsed / args.steps) / 1e9
     avg_main_ms = main_ms / max(1, n_sel)
     achieved = 4.0 * n_local / (avg_main_ms * 1e-3) / 1e9 if avg_main_ms > 0 else None
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if tj.get("log2n") == args.log2n and tj.get("family") == args.family:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_note = pmc_traffic("pmc_traffic.json", args.log2n, args.family)
 
     res = {
         "metric": "Gkeys/s exact k-th select, 2^30 int32 (1 GPU) / 2^33 (8 GPU); % HBM roofline",
@@ -591,6 +598,7 @@ def main():
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
+            "traffic_source": traffic_note,
             "algorithmic_bytes_per_launch": 4 * n_local,
             "avg_launch_ms": avg_main_ms,
         },

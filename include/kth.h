@@ -68,6 +68,10 @@ typedef struct kth_stats {
 
 const char *kth_strerror(int code);
 int kth_version(void);
+/* Hash of the sources this libkth.so was built from (16 hex digits; "unknown"
+ * outside the in-tree Makefile).  bench.py uses a PMC measurement only when it
+ * was taken on the same build. */
+const char *kth_build_id(void);
 int kth_device_count(void);
 
 /* --- one-shot entry point -------------------------------------------------
@@ -233,6 +237,11 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
                            int32_t *out);
 int kth_select_i32_sharded(const int32_t *const *dev_shards, const int64_t *shard_n, int ngpu, int64_t k,
                            int32_t *out);
+/* Diagnostics: host microseconds the last kth_sharded_select_i32 on h spent
+ * enqueueing device work and collectives for every device (from its entry to
+ * the last kth_dist_result enqueue; the wait for the answer excluded); -1 for
+ * a NULL handle. */
+double kth_sharded_enqueue_us(const kth_sharded *h);
 
 #ifdef __cplusplus
 }

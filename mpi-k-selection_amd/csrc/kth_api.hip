@@ -40,6 +40,7 @@ double window_z() {
 }
 constexpr int LEVEL_GRID_MAX = 1024;
 constexpr int POST_DENSE_GRID = 256;  // the candidates need ~100 dense WGs; the rare fallback streams the input with 256
+constexpr int HEAD_GRID_MAX = 64;  // k_head workgroups at most: 2^20 sample keys / (16 chunks of 1024 a workgroup)
 int gather_grid(u64 nchunks) {
     const u64 per_wg = (u64)(kth::DENSE_BLK / kth::WAVE) * kth::GATHER_BATCH;  // chunks per workgroup round
     return (int)std::max<u64>(1, (nchunks + per_wg - 1) / per_wg);
@@ -83,10 +84,12 @@ struct kth_ctx {
     int device = 0;
     int main_grid[5] = {0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
     bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
+    bool fault_barrier = false;    // KTH_FAULT_BARRIER (tests): k_finish reports a grid-barrier timeout
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
     bool coop = true;          // window / radix paths as k_head + k_main + k_finish (KTH_COOP=0: per-level launches)
+    bool coop_resident = true; // the cooperative grids fit the device at once (occupancy check at ctx creation)
     int fin_grid = 256;        // k_finish workgroups (one per CU; KTH_FIN_GRID)
     uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
     int fin_set = 0;           // k_finish slot set of the next launch (the other one is cleared by it)
@@ -117,6 +120,7 @@ struct kth_ctx {
     bool dist_zero = false;  // sharded: the bound slots still need clearing
     bool dist_open = false;  // sharded: begun, kth_dist_result not yet enqueued
     bool dist_coop_window = false;  // sharded: the window came from k_head (state carried, no pick left)
+    bool counts_left = false;  // a cooperative window select left islot(1) / cand_count for the next k_head to clear
     // KTH_STAMPS=1 diagnostics: per-launch [WG][8] wall-clock stamps, dumped after each select
     u64 *stamps = nullptr;
     int stamp_next = 0;
@@ -335,6 +339,7 @@ kth::CoopArgs coop_args(kth_ctx *c, u64 slot_off, int32_t *d_out, int32_t *d_sta
     x.dense_per_wg = DENSE_PER_WG;
     x.sparse_per_wg = FIN_SPARSE_PER_WG;
     x.slack64 = c->head_slack64;
+    x.fault = c->fault_barrier ? 1u : 0u;
     return x;
 }
 
@@ -437,6 +442,7 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
         a.n_local = (u64)n;
         launch_finish(c, a, d_out, d_status);
         c->last_state = 0;
+        c->counts_left = true;  // (k_head clears them; a sharded select on this ctx must too)
         return launch_check();
     }
     // sample + first digit of the sample
@@ -582,6 +588,11 @@ const char *kth_strerror(int code) {
 
 int kth_version(void) { return KTH_VERSION; }
 
+#ifndef KTH_BUILD_ID
+#define KTH_BUILD_ID "unknown"
+#endif
+const char *kth_build_id(void) { return KTH_BUILD_ID; }
+
 int kth_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -649,6 +660,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
             // so its count pass must report the bracket failure
             c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
+            c->fault_barrier = getenv("KTH_FAULT_BARRIER") != nullptr;
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
@@ -676,6 +688,29 @@ int kth_ctx_create(int device, kth_ctx **out) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)FIN_DYN_LDS) != hipSuccess)
             c->coop = false;  // no LDS-resident finish: per-level launches
         (void)hipGetLastError();
+        // The grid barriers of k_head / k_finish need every workgroup resident
+        // at once.  Their grids are sized for that (k_finish: one 1024-thread
+        // workgroup per CU with ~145 KiB of LDS; k_head: at most 64
+        // workgroups); check it against the occupancy query once, and refuse
+        // the cooperative path when the device cannot hold the grid (a plain
+        // launch checks nothing).  Residency can still be taken away at run
+        // time by other streams or processes: the spins are bounded, a timeout
+        // is reported (state error ERR_BARRIER, d_out untouched) and the
+        // synchronous entry points redo the select on the per-level path.
+        {
+            int fin_per_cu = 0, head_per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&fin_per_cu, reinterpret_cast<const void *>(kth::k_finish),
+                                                             kth::DENSE_BLK, FIN_DYN_LDS) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&head_per_cu, reinterpret_cast<const void *>(kth::k_head),
+                                                             kth::DENSE_BLK, 0) != hipSuccess)
+                fin_per_cu = head_per_cu = -1;  // query unavailable: trust the static sizing
+            (void)hipGetLastError();
+            if (fin_per_cu >= 0 &&
+                ((int64_t)fin_per_cu * c->num_cu < c->fin_grid || (int64_t)head_per_cu * c->num_cu < HEAD_GRID_MAX)) {
+                c->coop = false;
+                c->coop_resident = false;
+            }
+        }
     } while (0);
     if (rc != KTH_OK) {
         kth_ctx_destroy(c);
@@ -757,7 +792,22 @@ int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, in
     KTH_TRY(select_async(c, dk, n, k, nullptr, c->d_status));
     HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->h_status[1] != 0) return KTH_EINTERNAL;
+    if (c->h_status[1] == (int32_t)kth::ERR_BARRIER && c->coop) {
+        // a cooperative grid was not co-resident (another stream or process
+        // held CUs): redo the select on the per-level path, which needs no
+        // residency; the slots are re-zeroed first (dirty)
+        c->dirty = true;
+        c->coop = false;
+        const int rc = select_async(c, dk, n, k, nullptr, c->d_status);
+        c->coop = true;
+        KTH_TRY(rc);
+        HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (c->h_status[1] != 0) {
+        c->dirty = true;
+        return KTH_EINTERNAL;
+    }
     *out = c->h_status[0];
     return KTH_OK;
 }
@@ -1016,9 +1066,15 @@ int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     c->dist_level_next = 0;
     c->dist_zero = true;  // kth_dist_sample clears the slots inside its kernel
     // the ctx's own slots are left zeroed by every completed k_result; a
-    // sequence cut short (dirty, or a dist selection never finished) re-zeroes
-    if (c->dirty || c->dist_open) HIP_TRY(hipMemsetAsync(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64), c->stream));
+    // sequence cut short (dirty, or a dist selection never finished) re-zeroes,
+    // and so does a cooperative single-GPU window select, which leaves its
+    // count slot and candidate count for its next k_head to clear (the
+    // streaming pass would append after a stale count, and the candidate
+    // levels would histogram the previous select's keys)
+    if (c->dirty || c->dist_open || c->counts_left)
+        HIP_TRY(hipMemsetAsync(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64), c->stream));
     c->dirty = false;
+    c->counts_left = false;
     c->dist_open = true;
     return KTH_OK;
 }

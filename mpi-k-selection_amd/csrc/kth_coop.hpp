@@ -43,6 +43,7 @@ struct CoopArgs {
     u64 zero2_words;
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
     uint32_t sample_ready;  // k_head: the sample (order keys) is already in `sample` (sharded window)
+    uint32_t fault;    // test hook (KTH_FAULT_BARRIER): the first grid barrier reports a timeout
 };
 
 // This wave's outstanding global accesses (atomics, write-through stores) are
@@ -313,7 +314,10 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         SelState o = ss;
-        if (!ok && !o.error) {
+        // a timed-out barrier of any workgroup (consumed here, so that a
+        // sharded window -- k_head without a k_finish -- leaves no flag behind)
+        const uint32_t berr = __hip_atomic_exchange(x.bar + BAR_ERR, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((!ok || berr) && !o.error) {
             o.error = ERR_BARRIER;
             o.mode = MODE_DONE;
         } else if (o.mode == MODE_SAMPLE && !o.error) {
@@ -692,6 +696,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
             hist_flush<DENSE_BLK>(lh, plan, slot);
         if (L == 0) KTH_STAMP(a, 2);
         grid_sync(gb, s_base, ok);
+        if (x.fault) ok = false;  // test hook: as if this barrier had timed out
         if (L == 0) KTH_STAMP(a, 3);
         if (copies > 1)
             pick_slot_copies<DENSE_BLK>(ss, slot, nb, copies, reinterpret_cast<u64 *>(&lh[0][0]), scratch, &s_cnt0);
@@ -715,7 +720,10 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         if ((!ok || berr) && !o.error) o.error = ERR_BARRIER;
         if (o.mode != MODE_DONE && !o.error) o.error = 16 + o.mode;
         *a.st_out = o;
-        if (x.d_out) *x.d_out = i32_of_key(o.answer);
+        // only a verified answer reaches d_out: after a barrier timeout (a grid
+        // that was not co-resident) or a failed check d_out keeps its value and
+        // the error is in the state (kth_ctx_last_stats) and d_status[1]
+        if (x.d_out && !o.error) *x.d_out = i32_of_key(o.answer);
         if (x.d_status) {
             x.d_status[0] = i32_of_key(o.answer);
             x.d_status[1] = (int32_t)o.error;

@@ -928,7 +928,7 @@ __global__ __launch_bounds__(BLK) void k_result(StepArgs a, int32_t *d_out, int3
         SelState o = ss;
         if (o.mode != MODE_DONE && !o.error) o.error = 16 + o.mode;
         *a.st_out = o;
-        if (d_out) *d_out = i32_of_key(o.answer);
+        if (d_out && !o.error) *d_out = i32_of_key(o.answer);  // only a verified answer reaches d_out
         if (d_status) {
             d_status[0] = i32_of_key(o.answer);
             d_status[1] = (int32_t)o.error;
@@ -967,7 +967,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(const int32_t *__restrict
         done += d;
     }
     if (threadIdx.x == 0) {
-        if (d_out) d_out[0] = i32_of_key(prefix);
+        if (d_out && ok) d_out[0] = i32_of_key(prefix);
         if (d_status) {
             d_status[0] = i32_of_key(prefix);
             d_status[1] = ok ? 0 : 1;

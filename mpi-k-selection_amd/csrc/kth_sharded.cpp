@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -38,6 +39,7 @@ struct Rccl {
     ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
     ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Broadcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
 };
@@ -59,9 +61,10 @@ const Rccl &rccl() {
         x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
         x.AllReduce = reinterpret_cast<decltype(x.AllReduce)>(dlsym(h, "ncclAllReduce"));
         x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
+        x.Broadcast = reinterpret_cast<decltype(x.Broadcast)>(dlsym(h, "ncclBroadcast"));
         x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
         x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
-        x.ok = x.CommInitAll && x.CommDestroy && x.AllReduce && x.AllGather && x.GroupStart && x.GroupEnd;
+        x.ok = x.CommInitAll && x.CommDestroy && x.AllReduce && x.AllGather && x.Broadcast && x.GroupStart && x.GroupEnd;
         return x;
     }();
     return r;
@@ -119,6 +122,7 @@ int grow(int device, void **p, int64_t *cap, int64_t bytes) {
 
 struct kth_sharded {
     std::vector<Dev> d;
+    double enqueue_us = 0;  // host time of the last select up to its last enqueue (kth_sharded_enqueue_us)
 };
 
 namespace {
@@ -222,15 +226,31 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     }
     if (k < 1 || k > n_total) return KTH_EINVAL;
     if (n_min < SMALL_PER_GPU) return select_gathered(h, shards, shard_n, n_total, k, out);
+    const auto t0 = std::chrono::steady_clock::now();
 
     // ~kth_dist_sample_size(n_total) sample keys in all, split over the devices
-    // (as many per device: unbalanced shards only make the window a worse guess)
-    int64_t s = std::max<int64_t>(64, (kth_dist_sample_size(n_total) / P) & ~int64_t(63));
-    s = std::min<int64_t>(s, n_min & ~int64_t(63));
+    // in proportion to their shard sizes (a multiple of 64 each, at least 64, at
+    // most the shard): the gathered sample is then ~uniform over the union also
+    // for unbalanced shards, so the window is as good a guess as one GPU's.
+    // Balanced shards give every device the same count and one all-gather;
+    // unequal counts are gathered as one group of broadcasts (a gatherv).
+    const int64_t s_want = kth_dist_sample_size(n_total);
+    std::vector<int64_t> s_dev((size_t)P), s_off((size_t)P + 1, 0);
+    bool equal = true;
+    for (int i = 0; i < P; ++i) {
+        const double share = (double)s_want * (double)shard_n[i] / (double)n_total;
+        int64_t si = std::max<int64_t>(64, (int64_t)share & ~int64_t(63));
+        si = std::min<int64_t>(si, shard_n[i] & ~int64_t(63));
+        s_dev[(size_t)i] = si;
+        s_off[(size_t)i + 1] = s_off[(size_t)i] + si;
+        equal = equal && si == s_dev[0];
+    }
+    const int64_t s_total = s_off[(size_t)P];
     const Rccl &R = rccl();
-    for (Dev &x : h->d) {
-        TRY(grow(x.device, reinterpret_cast<void **>(&x.sample), &x.sample_cap, s * 4));
-        TRY(grow(x.device, reinterpret_cast<void **>(&x.gathered), &x.gathered_cap, s * 4 * P));
+    for (int i = 0; i < P; ++i) {
+        Dev &x = h->d[(size_t)i];
+        TRY(grow(x.device, reinterpret_cast<void **>(&x.sample), &x.sample_cap, s_dev[(size_t)i] * 4));
+        TRY(grow(x.device, reinterpret_cast<void **>(&x.gathered), &x.gathered_cap, s_total * 4));
     }
     auto allreduce = [&](int slot) -> int {
         NCCLT(R.GroupStart());
@@ -247,19 +267,29 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];
         TRY(kth_dist_begin(x.ctx, x.slots, n_total, k));
-        TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], x.sample, s));
+        TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], x.sample, s_dev[(size_t)i]));
     }
     NCCLT(R.GroupStart());
-    for (Dev &x : h->d)
-        if (R.AllGather(x.sample, x.gathered, (size_t)s, ncclUint32, x.comm, x.stream) != ncclSuccess) {
+    for (int i = 0; i < P; ++i) {
+        Dev &x = h->d[(size_t)i];
+        ncclResult_t r = ncclSuccess;
+        if (equal) {
+            r = R.AllGather(x.sample, x.gathered, (size_t)s_dev[0], ncclUint32, x.comm, x.stream);
+        } else {
+            for (int root = 0; root < P && r == ncclSuccess; ++root)
+                r = R.Broadcast(root == i ? x.sample : nullptr, x.gathered + s_off[(size_t)root],
+                                (size_t)s_dev[(size_t)root], ncclUint32, root, x.comm, x.stream);
+        }
+        if (r != ncclSuccess) {
             (void)R.GroupEnd();
             return KTH_ECOMM;
         }
+    }
     NCCLT(R.GroupEnd());
     int slot = -1;
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];
-        TRY(kth_dist_window(x.ctx, x.gathered, s * P));
+        TRY(kth_dist_window(x.ctx, x.gathered, s_total));
         const int r = kth_dist_scan(x.ctx, shards[i], shard_n[i]);
         TRY(r);
         slot = r;
@@ -274,6 +304,7 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
         TRY(allreduce(slot));
     }
     for (Dev &x : h->d) TRY(kth_dist_result(x.ctx, x.out));
+    h->enqueue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     // every device must hold the same answer (they picked the same digits from
     // the same reduced histograms); the per-device error words must be clear
     int32_t first = 0;
@@ -291,6 +322,8 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     *out = first;
     return KTH_OK;
 }
+
+double kth_sharded_enqueue_us(const kth_sharded *h) { return h ? h->enqueue_us : -1.0; }
 
 // One-shot form: shard i's device from its pointer; the handle (RCCL
 // communicators, per-device ctx and scratch) is kept per host thread and

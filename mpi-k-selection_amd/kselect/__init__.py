@@ -40,6 +40,8 @@ from ._lib import (  # noqa: F401
     KthLibraryMissing,
     KthStats,
     check,
+    check_single_runtime,
+    hip_runtimes,
     load,
     strerror,
 )
@@ -122,6 +124,8 @@ class Selector:
         return self._ctx
 
     def set_stream(self, stream):
+        if stream is not None and not isinstance(stream, int):
+            check_single_runtime()  # a torch stream handle is only meaningful to torch's runtime
         check(LIB.kth_ctx_set_stream(self._ctx, _stream_handle(stream)), "kth_ctx_set_stream")
 
     def sync(self):
@@ -227,6 +231,10 @@ class ShardedSelector:
         out = ctypes.c_int32()
         check(LIB.kth_sharded_select_i32(self._h, ptrs, ns, int(k), ctypes.byref(out)), "kth_sharded_select_i32")
         return out.value
+
+    def enqueue_us(self):
+        """Host microseconds the last select spent enqueueing (kth_sharded_enqueue_us)."""
+        return LIB.kth_sharded_enqueue_us(self._h)
 
     def close(self):
         if self._h:

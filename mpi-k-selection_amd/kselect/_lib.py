@@ -74,6 +74,7 @@ PROTOS = {
     # kth.h
     "kth_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "kth_version": (ctypes.c_int, []),
+    "kth_build_id": (ctypes.c_char_p, []),
     "kth_device_count": (ctypes.c_int, []),
     "kth_select_i32": (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int64, c_i32p]),
     "kth_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_vp)]),
@@ -111,6 +112,7 @@ PROTOS = {
     "kth_sharded_destroy": (ctypes.c_int, [c_vp]),
     "kth_sharded_select_i32": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_i32p]),
     "kth_select_i32_sharded": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int64, c_i32p]),
+    "kth_sharded_enqueue_us": (ctypes.c_double, [c_vp]),
     # vector.h
     "VecNew": (IntVectorPtr, [ctypes.c_int]),
     "VecAdd": (ctypes.c_int, [IntVectorPtr, ctypes.c_int]),
@@ -136,8 +138,41 @@ PROTOS = {
 _lib = None
 
 
+def hip_runtimes():
+    """Distinct HIP runtime files (libamdhip64) mapped into this process."""
+    found = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.rsplit(None, 1)[-1] if "/" in line else ""
+                if "libamdhip64" in os.path.basename(path):
+                    found.add(os.path.realpath(path))
+    except OSError:
+        pass
+    return sorted(found)
+
+
+def check_single_runtime():
+    """Raise if two HIP runtimes are loaded.  Streams, events and the null
+    stream of one runtime mean nothing to the other: work libkth.so enqueues
+    would not be ordered against torch's streams (a .item() could read an
+    answer buffer before the select that writes it), and a torch stream handle
+    passed to libkth.so would be an invalid handle."""
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise RuntimeError(
+            "two HIP runtimes are loaded in this process (" + ", ".join(rts) + "); "
+            "import torch before libkth.so is loaded (kselect does this itself when torch is importable)")
+
+
 def load():
-    """Load libkth.so once; raise KthLibraryMissing if it is not built."""
+    """Load libkth.so once; raise KthLibraryMissing if it is not built.
+
+    torch (when importable) is imported first: libkth.so needs the HIP runtime
+    by its soname (libamdhip64.so.7), which then binds to the copy torch has
+    already loaded, so the process holds ONE HIP runtime and libkth.so's
+    streams and torch's are the same objects.  Loaded the other way round, torch
+    would add its bundled runtime next to /opt/rocm's (check_single_runtime)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -145,7 +180,12 @@ def load():
         raise KthLibraryMissing(
             f"libkth.so not found at {LIB_PATH}; build it with `make -C {PKG_ROOT}` "
             "(there is no CPU fallback)")
+    try:
+        import torch  # noqa: F401 -- see the docstring: one HIP runtime per process
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
+    check_single_runtime()
     for name, (res, args) in PROTOS.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -29,7 +29,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check
+from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check, check_single_runtime
 from .rccl import RcclComm, TorchComm
 
 SMALL_PER_RANK = 64  # below this many keys per rank: all-gather and select locally
@@ -46,6 +46,7 @@ class HipBackend:
     """Per-rank device steps through the kth_dist_* entry points of libkth.so."""
 
     def __init__(self, device, selector=None):
+        check_single_runtime()  # torch's streams and RCCL must share libkth.so's HIP runtime
         self.device = torch.device("cuda", device)
         self.sel = selector or Selector(device)
         self.stream = torch.cuda.current_stream(self.device)

@@ -212,3 +212,33 @@ def test_protocol_constants_exported(lib):
     assert lib.kth_dist_cand_capacity(1000) == 1 << 20
     idx = cb.sample_indices(1 << 24, (1 << 18) + 64)  # 257 chunks, the last one partial
     assert idx.size == (1 << 18) + 64 and idx[1024] == (1 << 24) // 257 and idx[-1] == 256 * ((1 << 24) // 257) + 63
+
+
+@pytest.mark.parametrize("first", ["kselect", "torch"])
+def test_one_hip_runtime_whatever_the_import_order(first):
+    """libkth.so and torch share ONE HIP runtime in a process, whichever is
+    imported first.  libkth.so needs libamdhip64.so.7 by soname; torch bundles
+    its own copy under that soname.  Loaded before torch, libkth.so used to pull
+    /opt/rocm's runtime and torch then added its own: two null streams, so a
+    torch .item() was not ordered after libkth's kernels (a world-1
+    DistSelector read the previous select's answer) and torch stream handles
+    were invalid in libkth (kth_dist_sample: HIP runtime error).  kselect now
+    imports torch before loading the library and refuses a second runtime."""
+    second = "torch" if first == "kselect" else "kselect"
+    code = (f"import sys; sys.path.insert(0, {PKG!r}); import {first}; import {second}; import kselect; "
+            "print(len(kselect.hip_runtimes())); kselect.check_single_runtime()")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.split()[-1] == "1", p.stdout
+
+
+def test_second_hip_runtime_is_refused():
+    """A process that loaded /opt/rocm's runtime through libkth.so before torch
+    (bypassing kselect) holds two runtimes; kselect's check names them."""
+    rocm = "/opt/rocm/lib/libamdhip64.so.7"
+    if not os.path.exists(rocm):
+        pytest.skip("no /opt/rocm runtime")
+    code = (f"import ctypes, sys; ctypes.CDLL({LIB!r}); import torch; sys.path.insert(0, {PKG!r}); "
+            "import kselect")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    assert p.returncode != 0 and "two HIP runtimes" in p.stderr, p.stderr[-2000:]

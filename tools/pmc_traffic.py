@@ -9,7 +9,11 @@ averaged over the kernel's dispatches and reported per launch.
 """
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-k-selection_amd"))
+import kselect  # noqa: E402  (only for the build id of the library the counters were taken on)
 
 
 def per_dispatch(path, kernel, counter):
@@ -42,6 +46,7 @@ res = {
     "hbm_bytes_per_launch": read_bytes + write_bytes,
     "algorithmic_bytes_per_launch": algo,
     "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
+    "build_id": kselect.LIB.kth_build_id().decode(),
     "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads), write = WRITE_SIZE",
 }
 json.dump(res, open(out, "w"), indent=1)
