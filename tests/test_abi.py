@@ -12,7 +12,7 @@ import pytest
 
 from conftest import PKG, REPO
 
-LIB = os.path.join(PKG, "lib", "libkth.so")
+LIB = os.environ.get("KTH_LIB") or os.path.join(PKG, "lib", "libkth.so")
 REF_VEC = os.path.join(REPO, "oracle", "_ref", "libvector_ref.so")
 
 

@@ -16,7 +16,7 @@ import pytest
 
 from conftest import GOLDEN, PKG
 
-BIN = os.path.join(PKG, "bin", "kth_cgm")
+BIN = os.path.join(os.environ.get("KTH_BIN_DIR") or os.path.join(PKG, "bin"), "kth_cgm")
 MPIRUN = "/opt/conda/bin/mpirun"
 OUT = re.compile(r"kth element=(-?\d+) \ntime: ([0-9.]+)\n")
 

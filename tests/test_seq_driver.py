@@ -14,7 +14,7 @@ import pytest
 
 from conftest import PKG
 
-BIN = os.path.join(PKG, "bin", "kth_seq")
+BIN = os.path.join(os.environ.get("KTH_BIN_DIR") or os.path.join(PKG, "bin"), "kth_seq")
 OUT = re.compile(r"Solution found solution=(-?\d+) \ntime: ([0-9.]+)\n")
 
 
