@@ -62,6 +62,7 @@ constexpr u64 FIN_SPARSE_PER_WG = (u64)kth::DENSE_BLK * kth::FIN_UNROLL * 4;  //
 constexpr double HEAD_SLACK = 1.5;  // k_head early window (EarlyWindow); KTH_HEAD_SLACK overrides, 0 = off
 static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
+constexpr u64 TK_STAGE_MAX_FRAC = 32;  // staged top-k (k_main<5/6>) for k <= n / 32
 
 #define HIP_TRY(x)                                                                                    \
     do {                                                                                              \
@@ -82,9 +83,11 @@ constexpr int MAX_EVENTS = 4 * 2048;
 
 struct kth_ctx {
     int device = 0;
-    int main_grid[5] = {0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
+    int main_grid[7] = {0, 0, 0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
     bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
     bool fault_barrier = false;    // KTH_FAULT_BARRIER (tests): k_finish reports a grid-barrier timeout
+    bool topk_stage = true;        // staged top-k (k_main<5/6>); KTH_TOPK_STAGE=0 turns it off
+    u64 topk_seg_cap = 0;          // KTH_TOPK_SEG_CAP (tests): entries per staging segment (0 = sized from n)
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
@@ -104,6 +107,14 @@ struct kth_ctx {
     u64 cand_cap = 0;
     uint32_t *cand_rows = nullptr;  // k_main<3/4>: each candidate's 1024-key row (top-k)
     u64 cand_rows_cap = 0;
+    // k_main<5/6> (top-k): per-wave segments of staged keys + positions, per wave-row counts
+    int32_t *tk_segv = nullptr;
+    u64 tk_segv_cap = 0;
+    uint8_t *tk_segp = nullptr;
+    u64 tk_segp_cap = 0;
+    uint32_t *tk_wcnt = nullptr;
+    u64 tk_wcnt_cap = 0;
+    kth::TkSeg tk_seg{};  // the segments of the next launch_main<5/6>
     int32_t *staging = nullptr;
     u64 staging_cap = 0;
     u64 *topk = nullptr;  // top-k chunk counts, bases, [need, error]
@@ -395,12 +406,15 @@ int run_radix(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d_
 // The streaming pass, plain (tflag 0) or with the top-k records of k_main<tflag>.
 void launch_main(kth_ctx *c, const StepArgs &a, int tflag, uint32_t *tflags) {
     const int g = c->main_grid[tflag];
+    const kth::TkSeg none{};
     switch (tflag) {
-    case 1: kth::k_main<1><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr); break;
-    case 2: kth::k_main<2><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr); break;
-    case 3: kth::k_main<3><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows); break;
-    case 4: kth::k_main<4><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows); break;
-    default: kth::k_main<0><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr); break;
+    case 1: kth::k_main<1><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr, none); break;
+    case 2: kth::k_main<2><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr, none); break;
+    case 3: kth::k_main<3><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows, none); break;
+    case 4: kth::k_main<4><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, c->cand_rows, none); break;
+    case 5: kth::k_main<5><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr, c->tk_seg); break;
+    case 6: kth::k_main<6><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, tflags, nullptr, c->tk_seg); break;
+    default: kth::k_main<0><<<g, kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr, none); break;
     }
 }
 
@@ -630,13 +644,15 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // holds 512 / alloc(VGPR) waves, MI355X_MICROARCH.md register files);
             // the top-k variants keep more keys live and may allocate more VGPRs.
             // hipOccupancyMaxActiveBlocksPerMultiprocessor under-reports here.
-            const void *fns[5] = {reinterpret_cast<const void *>(kth::k_main<0>),
+            const void *fns[7] = {reinterpret_cast<const void *>(kth::k_main<0>),
                                   reinterpret_cast<const void *>(kth::k_main<1>),
                                   reinterpret_cast<const void *>(kth::k_main<2>),
                                   reinterpret_cast<const void *>(kth::k_main<3>),
-                                  reinterpret_cast<const void *>(kth::k_main<4>)};
+                                  reinterpret_cast<const void *>(kth::k_main<4>),
+                                  reinterpret_cast<const void *>(kth::k_main<5>),
+                                  reinterpret_cast<const void *>(kth::k_main<6>)};
             const char *e = getenv("KTH_MAIN_WG_PER_CU");
-            for (int v = 0; v < 5; ++v) {
+            for (int v = 0; v < 7; ++v) {
                 int per = 4;
                 hipFuncAttributes fa;
                 if (hipFuncGetAttributes(&fa, fns[v]) == hipSuccess && fa.numRegs > 0) {
@@ -661,6 +677,8 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // so its count pass must report the bracket failure
             c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
             c->fault_barrier = getenv("KTH_FAULT_BARRIER") != nullptr;
+            if (const char *g = getenv("KTH_TOPK_STAGE")) c->topk_stage = atoi(g) != 0;
+            if (const char *g = getenv("KTH_TOPK_SEG_CAP")) c->topk_seg_cap = (u64)std::max(0, atoi(g));
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
@@ -731,6 +749,9 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->sample) (void)hipFree(c->sample);
     if (c->cand) (void)hipFree(c->cand);
     if (c->cand_rows) (void)hipFree(c->cand_rows);
+    if (c->tk_segv) (void)hipFree(c->tk_segv);
+    if (c->tk_segp) (void)hipFree(c->tk_segp);
+    if (c->tk_wcnt) (void)hipFree(c->tk_wcnt);
     if (c->staging) (void)hipFree(c->staging);
     if (c->topk) (void)hipFree(c->topk);
     if (c->d_status) (void)hipFree(c->d_status);
@@ -945,10 +966,15 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     //   small that the rows holding output are a few per cent (k * 64 Ki <=
     //   n: one flag bit per row, the count pass loads only flagged tiles,
     //   tf 1 / 2; measured ~equal there, and it needs no alignment)
+    //   and for n / 64 Ki < k <= n / 32 (16-byte aligned), every key on the
+    //   kept side of the window's far edge staged in index order (tf 5 / 6):
+    //   neither the count nor the write pass reads the input (KTH_TOPK_STAGE=0: tf 3 / 4)
     const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
     const bool window = n > RADIX_MAX_N;
     const bool few = (u64)k * kth::TK_TILE * 64 <= (u64)n;
-    const int tf = (aligned && window && !few)             ? (largest ? 4 : 3)
+    const bool staged = aligned && window && !few && (u64)k * TK_STAGE_MAX_FRAC <= (u64)n && c->topk_stage;
+    const int tf = staged                                  ? (largest ? 6 : 5)
+                   : (aligned && window && !few)           ? (largest ? 4 : 3)
                    : (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1)
                                                              : 0;
     const u64 ncov = tf >= 3 ? nfull * kth::MAIN_UNROLL : 0;  // tiles = k_main rows (head == 0)
@@ -959,9 +985,19 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     const u64 foff = words - (fwords + 3) / 2 - 1;  // one spare u64: rounded up to 16 bytes
     uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + (foff + (foff & 1)));
     HIP_TRY(hipMemsetAsync(tflags, 0, 16, c->stream));  // window header: not valid until k_main<TF> runs
-    if (tf >= 3) {
+    if (tf == 3 || tf == 4) {
         KTH_TRY(reserve_cand(c, n));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->cand_rows), &c->cand_rows_cap, c->cand_cap));
+    }
+    u64 seg_cap = 0;
+    if (tf >= 5) {  // the staging segments: one per k_main wave, n / 16 entries in all
+        const u64 nwaves = (u64)c->main_grid[tf] * (kth::BLK / kth::WAVE);
+        seg_cap = c->topk_seg_cap ? c->topk_seg_cap : (std::max<u64>(1ull << 20, (u64)n / 16) + nwaves - 1) / nwaves;
+        KTH_TRY(reserve_cand(c, n));
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segv), &c->tk_segv_cap, seg_cap * nwaves * 4));
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segp), &c->tk_segp_cap, seg_cap * nwaves));
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_wcnt), &c->tk_wcnt_cap, ncov * (kth::BLK / kth::WAVE) * 4 + 16));
+        c->tk_seg = kth::TkSeg{c->tk_segv, c->tk_segp, (uint32_t)seg_cap, tflags + 3};
     }
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
     int64_t rank = largest ? n - k + 1 : k;
@@ -975,17 +1011,22 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     // count and write passes: one wave per 64 tiles
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
-    if (tf >= 3) {  // candidates' share first (atomics into zeroed counts), then the rows' words
+    if (tf >= 5) {  // the staged entries (rows < ncov), then the ragged rows from the input
+        kth::k_tk5_count<<<c->main_grid[tf], kth::TK_BLOCK, 0, c->stream>>>(c->tk_segv, seg_cap, tflags, nfull,
+                                                                            c->d_status, flip, c->tk_wcnt, tcnt);
+        kth::k_topk_count<true, 2><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                       tflags, head, nfull, sel_st, ncov);
+    } else if (tf >= 3) {  // candidates' share first (atomics into zeroed counts), then the rows' words
         HIP_TRY(hipMemsetAsync(tcnt, 0, ntiles * 4, c->stream));
         kth::k_topk_cands<<<c->num_cu * 8, kth::TK_BLOCK, 0, c->stream>>>(
             c->cand, c->cand_rows, cand_count(c), c->cand_cap / 4, c->d_status, flip, tcnt, tflags, sel_st);
-        kth::k_topk_count<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+        kth::k_topk_count<true, 1><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                           tcnt, tflags, head, nfull, sel_st, ncov);
     } else if (aligned) {
-        kth::k_topk_count<true, false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+        kth::k_topk_count<true, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                            tcnt, tflags, head, nfull, sel_st, 0);
     } else {
-        kth::k_topk_count<false, false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+        kth::k_topk_count<false, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                             tcnt, tflags, head, nfull, sel_st, 0);
     }
     if (getenv("KTH_TOPK_DEBUG")) {  // diagnostic: tile counts against a host recount
@@ -1022,7 +1063,14 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta,
                                                               c->st + c->last_state);
     kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
-    if (aligned)
+    if (tf >= 5) {
+        kth::k_tk5_write<<<c->main_grid[tf], kth::TK_BLOCK, 0, c->stream>>>(c->tk_segv, c->tk_segp, seg_cap, tflags,
+                                                                            nfull, c->d_status, flip, c->tk_wcnt, toff,
+                                                                            bbase, meta, d_vals, d_idx);
+        kth::k_topk_write<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+                                                                          tcnt, toff, bbase, meta, d_vals, d_idx,
+                                                                          tflags, ncov);
+    } else if (aligned)
         kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                     toff, bbase, meta, d_vals, d_idx);
     else
@@ -1156,7 +1204,7 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
-    kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr);
+    kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr, kth::TkSeg{});
     ev_main(c);
     c->dist_level_next = 0;
     KTH_TRY(launch_check());

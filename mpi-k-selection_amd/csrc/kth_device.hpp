@@ -215,6 +215,20 @@ __device__ __forceinline__ u64 wave_incl_scan64(u64 x) {
     return x;
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += dpp32<0x111, 0xF>(x);  // row_shr:1
+    x += dpp32<0x112, 0xF>(x);  // row_shr:2
+    x += dpp32<0x114, 0xF>(x);  // row_shr:4
+    x += dpp32<0x118, 0xF>(x);  // row_shr:8
+    x += dpp32<0x142, 0xA>(x);  // row_bcast:15
+    x += dpp32<0x143, 0xC>(x);  // row_bcast:31
+    return x;
+}
+
 // block_pick_vals for two targets at once (target t's histogram in h[t],
 // thread i owning bins [i*PER, i*PER + PER)): one wave scan per target, both
 // chains interleaved, and two barriers in all.  want[t] = false skips target

@@ -639,6 +639,102 @@ struct Stager {
     }
 };
 
+// TF 5 / 6 (top-k, k smallest / largest, n/65536 < k <= n/32): every key on
+// the kept side of the window's far edge (x <= hi / x >= lo: the keys certainly
+// in the output, the candidates and both edges) is staged IN INDEX ORDER with
+// its position in its wave-row (one byte) into the wave's own segment of the
+// top-k staging buffer -- segment g = the wave's global id, filled
+// sequentially: no atomics, no reservation.  The select's candidates (lo < x <
+// hi) are filtered out of the region into the candidate buffer when it is
+// flushed (the region holds raw int32 keys).  Per wave-row (the 256 keys of a
+// k_main row one wave loads), the staged count goes to the row words; the
+// top-k then never reads the input for those rows (k_tk5_count /
+// k_tk5_write).  A segment that overflows sets seg.ovf: the top-k then counts
+// and writes from the input (exact, slower).
+struct TkSeg {
+    int32_t *vals;  // nwaves * cap raw keys
+    uint8_t *pos;   // their positions in their wave-rows
+    uint32_t cap;   // entries per segment
+    uint32_t *ovf;  // set to 1 when any segment overflows
+};
+
+struct OrdStager {
+    static constexpr uint32_t CAP = ((uint32_t)WREG * 4 / 5) & ~63u;  // keys; CAP position bytes follow
+    uint32_t *reg;
+    uint32_t wfill;      // wave-uniform
+    uint32_t seg_fill;   // wave-uniform: entries already in the segment
+    u64 winside;         // wave-uniform: candidates seen
+    u64 seg_base;        // this wave's segment (entries)
+    int32_t slo, shi;
+    u64 *cand_count, *acc, cap;
+    uint32_t *cand_out;
+    TkSeg seg;
+
+    __device__ __forceinline__ void flush() {
+        const int lane = threadIdx.x & (WAVE - 1);
+        __builtin_amdgcn_wave_barrier();
+        const uint8_t *pb = reinterpret_cast<const uint8_t *>(reg + CAP);
+        const u64 base = seg_base + seg_fill;
+        for (uint32_t i = lane; i < wfill; i += WAVE)
+            if (seg_fill + i < seg.cap) {
+                seg.vals[base + i] = (int32_t)reg[i];
+                seg.pos[base + i] = pb[i];
+            }
+        if (seg_fill + wfill > seg.cap && lane == 0) *seg.ovf = 1u;
+        // the window's candidates -> the candidate buffer (one reservation)
+        uint32_t nin = 0;
+        for (uint32_t i0 = 0; i0 < wfill; i0 += WAVE) {
+            const int32_t x = (int32_t)reg[(i0 + lane) < wfill ? i0 + lane : 0];
+            nin += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(i0 + lane < wfill && x > slo && x < shi));
+        }
+        if (nin) {
+            const u64 g = reserve_cands(cand_count, acc, cap, nin);
+            uint32_t o = 0;
+            for (uint32_t i0 = 0; i0 < wfill; i0 += WAVE) {
+                const int32_t x = (int32_t)reg[(i0 + lane) < wfill ? i0 + lane : 0];
+                const bool in = i0 + lane < wfill && x > slo && x < shi;
+                const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
+                const uint32_t below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+                if (in && g + o + below < cap) put_cand(&cand_out[g + o + below], (uint32_t)x ^ 0x80000000u);
+                o += (uint32_t)__popcll(B);
+            }
+            winside += nin;
+        }
+        seg_fill += wfill;
+        wfill = 0;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // One wave-row slot: this lane's 4 consecutive keys q (positions p0 .. p0 + 3
+    // of the wave-row), f = the keys to stage (bit j: key j).  Appends them in
+    // index order; returns the wave's count (wave-uniform).
+    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t f, uint32_t p0) {
+        const uint32_t c = (uint32_t)__popc(f);
+        if (__builtin_amdgcn_ballot_w64(c != 0) == 0) return 0u;  // wave-uniform
+        const uint32_t incl = wave_incl_scan32(c);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        if (wfill + total > CAP) flush();
+        uint32_t at = wfill + incl - c;
+        uint8_t *pb = reinterpret_cast<uint8_t *>(reg + CAP);
+        if (f & 1u) { reg[at] = q.x; pb[at] = (uint8_t)p0; ++at; }
+        if (f & 2u) { reg[at] = q.y; pb[at] = (uint8_t)(p0 + 1); ++at; }
+        if (f & 4u) { reg[at] = q.z; pb[at] = (uint8_t)(p0 + 2); ++at; }
+        if (f & 8u) { reg[at] = q.w; pb[at] = (uint8_t)(p0 + 3); }
+        wfill += total;
+        return total;
+    }
+};
+static_assert(OrdStager::CAP + OrdStager::CAP / 4 <= (uint32_t)WREG && OrdStager::CAP >= 4 * WAVE,
+              "OrdStager region: keys + position bytes in one wave's region, >= one wave-row");
+
+// the 4 keys of q a TF 5 / 6 pass stages (x <= hi / x >= lo), as bits
+template <int TF>
+__device__ __forceinline__ uint32_t ord_flags(const uint4 &q, int32_t slo, int32_t shi, uint32_t valid4 = 0xFu) {
+    auto f1 = [&](uint32_t x) { return TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo; };
+    return ((f1(q.x) ? 1u : 0u) | (f1(q.y) ? 2u : 0u) | (f1(q.z) ? 4u : 0u) | (f1(q.w) ? 8u : 0u)) & valid4;
+}
+
 // Count and stage K keys of this lane (key j valid iff bit j of `valid`).  The
 // keys are the raw int32 words: signed compares against the signed window
 // bounds order them exactly like the order-preserving keys (no per-key xor);
@@ -699,13 +795,15 @@ static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot
 static_assert(BLK / WAVE == 4, "k_main<TF> stores one flag byte per wave, four per tile (tk_row_flagged's mask)");
 template <int TF>
 __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__ cand_out,
-                                              uint32_t *__restrict__ tflags, uint32_t *__restrict__ cand_rows) {
+                                              uint32_t *__restrict__ tflags, uint32_t *__restrict__ cand_rows,
+                                              TkSeg seg) {
     constexpr int U = MAIN_UNROLL, S = MAIN_SUB, K = 4 * S;
 #ifdef KTH_DIAG_NOROWS  // diagnostic builds only (wrong top-k results): cost of the row tags
     constexpr bool ROWS = false;
 #else
-    constexpr bool ROWS = TF >= 3;
+    constexpr bool ROWS = TF == 3 || TF == 4;
 #endif
+    constexpr bool ORD = TF >= 5;  // index-ordered staging of the kept side (OrdStager)
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
@@ -748,10 +846,25 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         }
     }
     Stager<ROWS> st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out, cand_rows};
+    OrdStager os{region[wid], 0u, 0u, 0ull, ((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.cap, slo, shi,
+                 a.cand_count, a.stats_acc, a.cap, cand_out, seg};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
+    // TF 5 / 6: the counts of 4 keys (as scan_keys) and their ordered staging
+    auto ord_keys = [&](const uint4 &q, uint32_t valid4, uint32_t p0) -> uint32_t {
+        const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t x = (int32_t)k4[j];
+            const bool ok = (valid4 >> j) & 1u;
+            clt += (ok & (x < slo)) ? 1u : 0u;
+            ceqlo += (ok & (x == slo)) ? 1u : 0u;
+            ceqhi += (ok & (x == shi)) ? 1u : 0u;
+        }
+        return os.row(q, ord_flags<TF>(q, slo, shi, valid4), p0);
+    };
 
     // a tile is consumed in groups of 4 * MAIN_SUB keys
-    constexpr int RW = TF >= 3 ? TF : 0;
+    constexpr int RW = (TF == 3 || TF == 4) ? TF : 0;
     auto scan_tile = [&](const uint4 (&x)[U], u64 t, RowAcc &ra) {
         static_assert(RW == 0 || U == S, "row tallies: one key group per tile");
 #pragma unroll
@@ -845,8 +958,23 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         load_tile(x, t);
         if constexpr (TF >= 3)
             if (pend_at != ~0ull) tflags[pend_at] = pend_word;  // the previous tile's words (lanes 0..U-1)
-        scan_tile(x, t, ra);
-        flag_tile(x, t, ra, e0, c0);
+        if constexpr (ORD) {
+            // row u: this lane's keys 4 * lane .. + 3 of the wave's 256 (its wave-row);
+            // lane u keeps row u's staged count for the row words
+            uint32_t rw = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t tot = ord_keys(x[u], 0xFu, 4u * (uint32_t)lane);
+                rw = lane == u ? tot : rw;
+            }
+            if (lane < U) {
+                pend_word = rw;
+                pend_at = 4 + ((t * U + lane) * (BLK / WAVE) + wid);
+            }
+        } else {
+            scan_tile(x, t, ra);
+            flag_tile(x, t, ra, e0, c0);
+        }
     }
     if constexpr (TF >= 3)
         if (pend_at != ~0ull) tflags[pend_at] = pend_word;
@@ -867,13 +995,24 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 kk[4 * u + 3] = x.w;
                 ok |= in ? (0xFu << (4 * u)) : 0u;
             }
-            scan_keys<K, false>(kk, ok, slo, shi, clt, ceqlo, ceqhi, st);
+            if constexpr (ORD) {  // (rows past k_main's full tiles: staged for the candidates only)
+#pragma unroll
+                for (int u = 0; u < S; ++u)
+                    (void)ord_keys(make_uint4(kk[4 * u], kk[4 * u + 1], kk[4 * u + 2], kk[4 * u + 3]), (ok >> (4 * u)) & 0xFu,
+                                   0u);
+            } else {
+                scan_keys<K, false>(kk, ok, slo, shi, clt, ceqlo, ceqhi, st);
+            }
         }
     if (blockIdx.x == 0) {  // the < 4-key unaligned head and tail
         const bool okh = threadIdx.x < head, okt = threadIdx.x < n - tail0;
         const uint32_t kk[2] = {okh ? p[threadIdx.x] : 0u, okt ? p[tail0 + threadIdx.x] : 0u};
-        scan_keys<2, false>(kk, (okh ? 1u : 0u) | (okt ? 2u : 0u), slo, shi, clt, ceqlo, ceqhi, st);
+        if constexpr (ORD)
+            (void)ord_keys(make_uint4(kk[0], kk[1], 0u, 0u), (okh ? 1u : 0u) | (okt ? 2u : 0u), 0u);
+        else
+            scan_keys<2, false>(kk, (okh ? 1u : 0u) | (okt ? 2u : 0u), slo, shi, clt, ceqlo, ceqhi, st);
     }
+    if constexpr (ORD) os.flush();  // the wave's last entries (and its candidates, reserved by the wave)
     // counts: wave reduce -> LDS -> one atomic per workgroup and counter; the
     // waves' final region fills are combined the same way, so the candidate
     // buffer sees one reservation per workgroup at the end of the pass
@@ -888,8 +1027,8 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         red[0][wid] = r0;
         red[1][wid] = r1;
         red[2][wid] = r2;
-        red[3][wid] = st.winside;
-        red[4][wid] = st.wfill;
+        red[3][wid] = ORD ? os.winside : st.winside;
+        red[4][wid] = ORD ? 0u : st.wfill;
     }
     __syncthreads();
     if (threadIdx.x < 5) {
@@ -908,7 +1047,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         }
     }
     __syncthreads();
-    if (st.wfill) {  // this wave's final region, at its share of the reservation
+    if (!ORD && st.wfill) {  // this wave's final region, at its share of the reservation
         u64 g = red[5][0];
         for (int w = 0; w < wid; ++w) g += red[4][w];
         st.put(g, st.wfill);

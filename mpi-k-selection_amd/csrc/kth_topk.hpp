@@ -31,19 +31,6 @@ constexpr int TK_TILES_PER_BLOCK = TK_BLOCK * 16;  // reduce / down-sweep granul
 // order test against the k-th key: flip = 0 for smallest, ~0 for largest
 __device__ __forceinline__ bool tk_better(uint32_t u, uint32_t uv, uint32_t flip) { return (u ^ flip) < (uv ^ flip); }
 
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
-}
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
-    x += dpp32<0x111, 0xF>(x);  // row_shr:1
-    x += dpp32<0x112, 0xF>(x);  // row_shr:2
-    x += dpp32<0x114, 0xF>(x);  // row_shr:4
-    x += dpp32<0x118, 0xF>(x);  // row_shr:8
-    x += dpp32<0x142, 0xA>(x);  // row_bcast:15
-    x += dpp32<0x143, 0xC>(x);  // row_bcast:31
-    return x;
-}
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(x), WAVE - 1);
 }
@@ -75,7 +62,16 @@ __device__ __forceinline__ bool tk_meta_ok(const uint32_t *tflags, const int32_t
 __device__ __forceinline__ uint32_t tk_better_of(uint32_t c) { return c & 0xFFFFu; }
 __device__ __forceinline__ uint32_t tk_equal_of(uint32_t c) { return (c >> 16) & 0x7FFFu; }
 
-template <bool ALIGNED, bool META>
+// STAGED (after k_main<5/6>): the first ncov tiles' staged entries hold every
+// key on the kept side of the window's far edge, in index order per wave-row;
+// when v lies inside the window and no segment overflowed, k_tk5_count /
+// k_tk5_write handle those tiles from the entries alone.
+__device__ __forceinline__ bool tk5_ok(const uint32_t *tflags, const int32_t *d_v) {
+    return tflags[2] == 1u && tflags[3] == 0u && d_v[0] >= (int32_t)tflags[0] && d_v[0] <= (int32_t)tflags[1];
+}
+
+// MODE: 0 = flags (k_main<1/2>) or none, 1 = row words (k_main<3/4>), 2 = staged (k_main<5/6>)
+template <bool ALIGNED, int MODE>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          uint32_t *__restrict__ tcnt,
@@ -84,9 +80,11 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
+    constexpr bool META = MODE == 1;
     const bool skip_ok =
-        !META && tflags[2] == 1u && (flip == 0u ? d_v[0] <= (int32_t)tflags[1] : d_v[0] >= (int32_t)tflags[0]);
+        MODE == 0 && tflags[2] == 1u && (flip == 0u ? d_v[0] <= (int32_t)tflags[1] : d_v[0] >= (int32_t)tflags[0]);
     const bool meta_ok = META && tk_meta_ok(tflags, d_v, st);
+    const bool staged_ok = MODE == 2 && tk5_ok(tflags, d_v);
     const uint32_t mark = meta_ok ? TK_RECOUNT : 0u;
     const uint32_t *fw = tflags + 4;
     // each wave takes 64 tiles at a time: lane l tests tile tg + l's flags, the
@@ -94,6 +92,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE) * WAVE; tg < ntiles; tg += nw * WAVE) {
         const u64 tl = tg + lane;
         bool act = tl < ntiles;
+        if (staged_ok && tl < ncov) act = false;  // counted by k_tk5_count
         if (act && meta_ok && tl < ncov) {
             const uint4 w = reinterpret_cast<const uint4 *>(fw)[tl];
             if (((w.x | w.y | w.z | w.w) & TK_RECOUNT) == 0u) {
@@ -266,13 +265,14 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 // every kept key its slot in the tile's output range, which is contiguous:
 // [bb + min(be, need), + #better + #kept ties).  The pairs are staged in the
 // wave's LDS and written out coalesced.
-template <bool ALIGNED>
+template <bool ALIGNED, bool STAGED = false>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          const uint32_t *__restrict__ tcnt,
                                                          const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
                                                          const u64 *__restrict__ meta, int32_t *__restrict__ vals,
-                                                         int64_t *__restrict__ idx) {
+                                                         int64_t *__restrict__ idx,
+                                                         const uint32_t *__restrict__ tflags = nullptr, u64 ncov = 0) {
     __shared__ uint32_t s_val[TK_BLOCK / WAVE][TK_TILE];
     __shared__ uint16_t s_col[TK_BLOCK / WAVE][TK_TILE];
     if (meta[1]) return;
@@ -280,7 +280,9 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
+    const u64 t_from = STAGED && tk5_ok(tflags, d_v) ? ncov : 0;  // tiles below t_from: k_tk5_write
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + w) * WAVE; tg < ntiles; tg += nw * WAVE) {
+        if (tg + WAVE <= t_from) continue;  // wave-uniform
         // lane l: tile tg + l's bases and whether it holds output keys
         const u64 tl = tg + lane;
         uint32_t c_l = 0;
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
             bb_l = bbase[2 * blk] + (off & 0xFFFFFFFFull);
             be_l = bbase[2 * blk + 1] + (off >> 32);
         }
-        const bool act = tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need);
+        const bool act = tl >= t_from && (tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need));
         u64 todo = __ballot(act);
         while (todo) {
             const int src = __builtin_ctzll(todo);
@@ -357,6 +359,107 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                 if (idx) idx[start + r] = (int64_t)(t * TK_TILE + s_col[w][r]);
             }
             __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
+        }
+    }
+}
+
+// ------------------------------------------------ staged top-k (k_main<5/6>)
+// Both kernels run on k_main's grid: workgroup b walks the tiles k_main's
+// workgroup b streamed (t = b, b + G, ... < nfull), wave w its segment 4b + w,
+// whose entries are the wave's wave-rows' staged keys back to back in that
+// order (row words: counts).  Lane l takes one wave-row of each window of 64.
+
+// Per wave-row: #better | #equal << 16 -> wcnt; per row (the 4 wave-rows of
+// its 4 waves, summed through LDS) -> tcnt.  Entries are read, the input is not.
+__global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restrict__ segv, u64 seg_cap,
+                                                        const uint32_t *__restrict__ tflags, u64 nfull,
+                                                        const int32_t *__restrict__ d_v, uint32_t flip,
+                                                        uint32_t *__restrict__ wcnt, uint32_t *__restrict__ tcnt) {
+    __shared__ uint32_t part[TK_BLOCK / WAVE][WAVE];
+    if (!tk5_ok(tflags, d_v)) return;  // grid-uniform
+    const int32_t v = d_v[0];
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const u64 b = blockIdx.x, G = gridDim.x;
+    const u64 m = (nfull > b ? (nfull - 1 - b) / G + 1 : 0) * MAIN_UNROLL;  // this wave's wave-rows
+    const int32_t *sv = segv + (b * (TK_BLOCK / WAVE) + w) * seg_cap;
+    uint32_t carry = 0;
+    for (u64 j0 = 0; j0 < m; j0 += WAVE) {  // same trip count in the 4 waves
+        const u64 j = j0 + lane;
+        const bool valid = j < m;
+        const u64 r = (b + (j / MAIN_UNROLL) * G) * MAIN_UNROLL + j % MAIN_UNROLL;
+        const uint32_t c = valid ? tflags[4 + r * (TK_BLOCK / WAVE) + w] : 0u;
+        const uint32_t incl = wave_incl_scan32(c);
+        const uint32_t start = carry + incl - c;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        uint32_t nb = 0, ne = 0;
+        for (uint32_t e = 0; e < c; ++e) {
+            const int32_t x = sv[start + e];
+            nb += (flip == 0u ? x < v : x > v) ? 1u : 0u;
+            ne += x == v ? 1u : 0u;
+        }
+        const uint32_t word = nb | ne << 16;
+        if (valid) wcnt[r * (TK_BLOCK / WAVE) + w] = word;
+        part[w][lane] = word;
+        __syncthreads();
+        if (w == 0 && valid) tcnt[r] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+        __syncthreads();
+    }
+}
+
+// The ordered compaction of the staged entries: a kept entry's slot is
+// #better before it + min(#equal before it, need), as in k_topk_write; the
+// wave-row's bases are its row's (toff, bbase) plus the earlier waves' counts
+// in the row (wcnt), and the entries are in index order within the wave-row.
+__global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restrict__ segv,
+                                                        const uint8_t *__restrict__ segp, u64 seg_cap,
+                                                        const uint32_t *__restrict__ tflags, u64 nfull,
+                                                        const int32_t *__restrict__ d_v, uint32_t flip,
+                                                        const uint32_t *__restrict__ wcnt,
+                                                        const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
+                                                        const u64 *__restrict__ meta, int32_t *__restrict__ vals,
+                                                        int64_t *__restrict__ idx) {
+    if (!tk5_ok(tflags, d_v) || meta[1]) return;  // grid-uniform
+    const u64 need = meta[0];
+    const int32_t v = d_v[0];
+    const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const u64 b = blockIdx.x, G = gridDim.x;
+    const u64 m = (nfull > b ? (nfull - 1 - b) / G + 1 : 0) * MAIN_UNROLL;
+    const u64 sbase = (b * (TK_BLOCK / WAVE) + w) * seg_cap;
+    uint32_t carry = 0;
+    for (u64 j0 = 0; j0 < m; j0 += WAVE) {
+        const u64 j = j0 + lane;
+        const bool valid = j < m;
+        const u64 r = (b + (j / MAIN_UNROLL) * G) * MAIN_UNROLL + j % MAIN_UNROLL;
+        const uint32_t c = valid ? tflags[4 + r * (TK_BLOCK / WAVE) + w] : 0u;
+        const uint32_t incl = wave_incl_scan32(c);
+        const uint32_t start = carry + incl - c;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        if (c == 0) continue;
+        const u64 off = toff[r], blk = r / TK_TILES_PER_BLOCK;
+        u64 bb = bbase[2 * blk] + (off & 0xFFFFFFFFull), be = bbase[2 * blk + 1] + (off >> 32);
+        const uint4 wc = *reinterpret_cast<const uint4 *>(wcnt + r * (TK_BLOCK / WAVE));
+        const uint32_t wcs[4] = {wc.x, wc.y, wc.z, wc.w};
+#pragma unroll
+        for (int q = 0; q < TK_BLOCK / WAVE; ++q)
+            if (q < w) {
+                bb += wcs[q] & 0xFFFFu;
+                be += wcs[q] >> 16;
+            }
+        const u64 i0 = r * TK_TILE + (u64)w * (TK_TILE / (TK_BLOCK / WAVE));  // the wave-row's first key
+        for (uint32_t e = 0; e < c; ++e) {
+            const int32_t x = segv[sbase + start + e];
+            u64 pos = ~0ull;
+            if (flip == 0u ? x < v : x > v) {
+                pos = bb + (be < need ? be : need);
+                ++bb;
+            } else if (x == v) {
+                if (be < need) pos = bb + be;
+                ++be;
+            }
+            if (pos != ~0ull) {
+                if (vals) vals[pos] = x;
+                if (idx) idx[pos] = (int64_t)(i0 + segp[sbase + start + e]);
+            }
         }
     }
 }

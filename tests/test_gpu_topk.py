@@ -206,3 +206,68 @@ def test_topk_large_k_from_stream_counts(gpu, largest):
             np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k}")
             np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{name} k={k}")
             assert gpu.stats()["error"] == 0
+
+
+def _staged_cases(n, rng):
+    uni = rng.integers(-2 ** 31, 2 ** 31, size=n, dtype=np.int64).astype(np.int32)
+    yield "uniform", uni
+    yield "narrow", rng.integers(-300, 300, size=n).astype(np.int32)     # heavy ties on the window edges
+    yield "few", rng.integers(-3, 4, size=n).astype(np.int32)
+    spike = uni.copy()
+    spike[rng.random(n) < 0.4] = -99                                       # window miss at the median
+    yield "spike", spike
+    a = np.arange(n, dtype=np.int64)
+    yield "sorted_asc", (a - n // 2).astype(np.int32)                      # the kept side in a few segments
+    yield "sorted_desc", (n // 2 - a).astype(np.int32)
+
+
+@pytest.mark.parametrize("largest", [False, True])
+def test_topk_staged_index_order(gpu, largest):
+    """n / 65536 < k <= n / 32 on the window path, 16-byte aligned keys: the
+    streaming pass stages every key on the kept side of the window's far edge in
+    index order per wave-row, with its position, in per-wave segments
+    (k_main<5/6>), and the count and write passes read those entries, not the
+    input (k_tk5_count, k_tk5_write); the ragged tail past the full tiles is
+    counted and written from the input.  Against a stable argsort."""
+    import torch
+    n = (1 << 23) + 4099
+    rng = np.random.default_rng(41 + largest)
+    for name, a in _staged_cases(n, rng):
+        d = torch.from_numpy(a).cuda()
+        for k in (n // 65536 + 1, n // 1024, n // 256, n // 64, n // 32):
+            vals, idx = _run(gpu, d, n, k, largest)
+            want = _ref_idx(a, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k}")
+            np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{name} k={k}")
+            assert gpu.stats()["error"] == 0
+
+
+def test_topk_staged_segment_overflow_falls_back(gpu):
+    """Staging segments too small for the kept side (KTH_TOPK_SEG_CAP, a
+    test-only hook): the overflow flag sends the count and write passes back to
+    the input, and the result is the same."""
+    import os
+    import torch
+    import kselect
+    os.environ["KTH_TOPK_SEG_CAP"] = "300"
+    try:
+        small = kselect.Selector(0)
+    finally:
+        del os.environ["KTH_TOPK_SEG_CAP"]
+    n = (1 << 23) + 4099
+    rng = np.random.default_rng(53)
+    for name, a in _staged_cases(n, rng):
+        d = torch.from_numpy(a).cuda()
+        for largest in (False, True):
+            for k in (n // 1024, n // 64):
+                vals, idx = _run(small, d, n, k, largest)
+                want = _ref_idx(a, k, largest)
+                np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k} {largest}")
+                np.testing.assert_array_equal(vals.cpu().numpy(), a[want], err_msg=f"{name} k={k} {largest}")
+    small.close()
+
+
+@pytest.mark.parametrize("k", [1 << 20, 1 << 24])
+def test_topk_staged_full_size(gpu, k):
+    """2^28 keys, k in the staged range: the exact top-k properties."""
+    test_topk_full_size_properties(gpu, "uniform_full", k, False)
