@@ -488,6 +488,12 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
         asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
         const uint32_t ob = opaque(bin);
         const uint32_t hi_edge = opaque(bin << 24) | 0x00FFFFFFu;
+        // value-linear rows: vbin(v) <= B  <=>  !(fma(v, s, o) >= B + 1), the
+        // same fma as pass A and one compare (no clamp, no convert): for t in
+        // [0, 255] trunc(t) <= B iff t < B + 1; t < 0 lands in bin 0 and passes;
+        // bin 255 (B = 255) keeps every key, +inf included: the threshold is
+        // then NaN and the unordered compare is true
+        const float thr = opaque(ob == 255u ? __builtin_nanf("") : (float)(ob + 1u));
         // one loop per map (no per-key branch on it)
         auto stage_rows = [&](auto vm) __attribute__((always_inline)) {
             constexpr bool VM = decltype(vm)::value;
@@ -499,18 +505,42 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t x = key[4 * g + q];
                     if constexpr (VM)
-                        c[q] = vbin(__uint_as_float(x), s2, o2) <= ob;
+                        c[q] = !(__builtin_fmaf(__uint_as_float(x), s2, o2) >= thr);
                     else
                         c[q] = x <= hi_edge;
                     bc[q] = __ballot(c[q]);
                 }
-                if ((bc[0] | bc[1] | bc[2] | bc[3]) != 0) {  // wave-uniform
+                const unsigned long long any = bc[0] | bc[1] | bc[2] | bc[3];
+                const uint32_t colg = e0 + (uint32_t)(g * WAVE * 4);
+                // no lane stages two keys of the group (the usual case: ~80 of a
+                // row's 4096 keys are staged): the lane's key goes to slot
+                // staged + mbcnt(any), one pair of stores, selects instead of a
+                // ballot + mbcnt chain per key slot
+                const unsigned long long coll = (bc[0] & bc[1]) | ((bc[0] | bc[1]) & bc[2]) |
+                                                ((bc[0] | bc[1] | bc[2]) & bc[3]);
+                if (any != 0 && coll == 0) {  // wave-uniform
+                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)any, staged));
+                    // (selects on the ballots in asm: written as ?: the compiler turns
+                    // the chain into a lane-indexed load of key[] from scratch)
+                    uint32_t val = key[4 * g], q;
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(key[4 * g + 1]), "s"(bc[1]));
+                    asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(q) : "s"(bc[1]));
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(key[4 * g + 2]), "s"(bc[2]));
+                    asm("v_cndmask_b32_e64 %0, %1, 2, %2" : "=v"(q) : "v"(q), "s"(bc[2]));
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(key[4 * g + 3]), "s"(bc[3]));
+                    asm("v_cndmask_b32_e64 %0, %1, 3, %2" : "=v"(q) : "v"(q), "s"(bc[3]));
+                    if (c[0] || c[1] || c[2] || c[3]) {
+                        skey[pos] = val;
+                        scol[pos] = colg + q;
+                    }
+                    staged += (uint32_t)__popcll(any);
+                } else if (any != 0) {  // wave-uniform
                     uint32_t pos = staged;
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
                         pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bc[q] >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bc[q], pos));
-                    const uint32_t colg = e0 + (uint32_t)(g * WAVE * 4);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if (c[q]) {

@@ -1,5 +1,5 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel averages and the kernel
-timeline of the last selection (tools/gpu_check.sh)."""
+timeline of the last selection (or top-k call): prof_summary.py CSV [kernels in the timeline, default 8]."""
 import csv
 import sys
 from collections import defaultdict
@@ -15,7 +15,7 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
 ks = [r for r in rows if "kth::" in r["Kernel_Name"]]
 starts = [i for i, r in enumerate(ks) if "k_gather" in r["Kernel_Name"] or "k_head" in r["Kernel_Name"]]
 if starts:
-    seq = ks[starts[-1]:starts[-1] + 8]
+    seq = ks[starts[-1]:starts[-1] + (int(sys.argv[2]) if len(sys.argv) > 2 else 8)]
     t0 = int(seq[0]["Start_Timestamp"])
     for r in seq:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
