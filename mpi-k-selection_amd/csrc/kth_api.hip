@@ -63,6 +63,7 @@ constexpr double HEAD_SLACK = 1.5;  // k_head early window (EarlyWindow); KTH_HE
 static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
 constexpr u64 TK_STAGE_MAX_FRAC = 32;  // staged top-k (k_main<5/6>) for k <= n / 32
+constexpr int TK5_SPLIT = 4;            // workgroups per k_main workgroup in k_tk5_count / k_tk5_write (window-parallel)
 
 #define HIP_TRY(x)                                                                                    \
     do {                                                                                              \
@@ -114,6 +115,8 @@ struct kth_ctx {
     u64 tk_segp_cap = 0;
     uint32_t *tk_wcnt = nullptr;
     u64 tk_wcnt_cap = 0;
+    uint32_t *tk_wstart = nullptr;  // staged top-k: entries before each window, per wave
+    u64 tk_wstart_cap = 0;
     kth::TkSeg tk_seg{};  // the segments of the next launch_main<5/6>
     int32_t *staging = nullptr;
     u64 staging_cap = 0;
@@ -752,6 +755,7 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->tk_segv) (void)hipFree(c->tk_segv);
     if (c->tk_segp) (void)hipFree(c->tk_segp);
     if (c->tk_wcnt) (void)hipFree(c->tk_wcnt);
+    if (c->tk_wstart) (void)hipFree(c->tk_wstart);
     if (c->staging) (void)hipFree(c->staging);
     if (c->topk) (void)hipFree(c->topk);
     if (c->d_status) (void)hipFree(c->d_status);
@@ -978,18 +982,22 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
                    : (u64)k * kth::TK_TILE <= (u64)n ? (largest ? 2 : 1)
                                                              : 0;
     const u64 ncov = tf >= 3 ? nfull * kth::MAIN_UNROLL : 0;  // tiles = k_main rows (head == 0)
-    const u64 fwords = 4 + (tf >= 3 ? ncov * (kth::BLK / kth::WAVE) : nfull);
-    const u64 words = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2 + (fwords + 3) / 2 + 1;
+    // tflags: the header and TF 1 / 2's flag bytes after 4 words, TF >= 3's
+    // row words after TF_W0 (kth::row_word); 64-byte aligned, so that a wave's
+    // 8 row words fill one 32-byte sector
+    const u64 fwords = tf >= 3 ? kth::TF_W0 + ncov * (kth::BLK / kth::WAVE) : 4 + nfull;
+    const u64 fw64 = (fwords + 1) / 2, before = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2;
+    const u64 words = before + fw64 + 8;
     KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
-    // tflags 16-byte aligned (k_topk_count reads the wave-row words as uint4)
-    const u64 foff = words - (fwords + 3) / 2 - 1;  // one spare u64: rounded up to 16 bytes
-    uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + (foff + (foff & 1)));
+    const u64 foff = (before + 7) & ~7ull;  // + fw64 <= words
+    uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + foff);
     HIP_TRY(hipMemsetAsync(tflags, 0, 16, c->stream));  // window header: not valid until k_main<TF> runs
     if (tf == 3 || tf == 4) {
         KTH_TRY(reserve_cand(c, n));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->cand_rows), &c->cand_rows_cap, c->cand_cap));
     }
     u64 seg_cap = 0;
+    uint32_t nwin = 0;
     if (tf >= 5) {  // the staging segments: one per k_main wave, n / 16 entries in all
         const u64 nwaves = (u64)c->main_grid[tf] * (kth::BLK / kth::WAVE);
         seg_cap = c->topk_seg_cap ? c->topk_seg_cap : (std::max<u64>(1ull << 20, (u64)n / 16) + nwaves - 1) / nwaves;
@@ -997,7 +1005,11 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segv), &c->tk_segv_cap, seg_cap * nwaves * 4));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segp), &c->tk_segp_cap, seg_cap * nwaves));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_wcnt), &c->tk_wcnt_cap, ncov * (kth::BLK / kth::WAVE) * 4 + 16));
-        c->tk_seg = kth::TkSeg{c->tk_segv, c->tk_segp, (uint32_t)seg_cap, tflags + 3};
+        // per wave and window (TK5_WIN_TILES of its tiles): the entries staged before it
+        const u64 G = (u64)c->main_grid[tf];
+        nwin = (uint32_t)(((nfull + G - 1) / G + kth::TK5_WIN_TILES - 1) / kth::TK5_WIN_TILES);
+        KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_wstart), &c->tk_wstart_cap, nwaves * std::max(nwin, 1u) * 4));
+        c->tk_seg = kth::TkSeg{c->tk_segv, c->tk_segp, (uint32_t)seg_cap, tflags + 3, c->tk_wstart, nwin};
     }
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
     int64_t rank = largest ? n - k + 1 : k;
@@ -1012,8 +1024,9 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
     if (tf >= 5) {  // the staged entries (rows < ncov), then the ragged rows from the input
-        kth::k_tk5_count<<<c->main_grid[tf], kth::TK_BLOCK, 0, c->stream>>>(c->tk_segv, seg_cap, tflags, nfull,
-                                                                            c->d_status, flip, c->tk_wcnt, tcnt);
+        kth::k_tk5_count<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
+            c->tk_segv, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status, flip,
+            c->tk_wcnt, tcnt);
         kth::k_topk_count<true, 2><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                        tflags, head, nfull, sel_st, ncov);
     } else if (tf >= 3) {  // candidates' share first (atomics into zeroed counts), then the rows' words
@@ -1064,9 +1077,9 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
                                                               c->st + c->last_state);
     kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
     if (tf >= 5) {
-        kth::k_tk5_write<<<c->main_grid[tf], kth::TK_BLOCK, 0, c->stream>>>(c->tk_segv, c->tk_segp, seg_cap, tflags,
-                                                                            nfull, c->d_status, flip, c->tk_wcnt, toff,
-                                                                            bbase, meta, d_vals, d_idx);
+        kth::k_tk5_write<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
+            c->tk_segv, c->tk_segp, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status,
+            flip, c->tk_wcnt, tcnt, toff, bbase, meta, d_vals, d_idx);
         kth::k_topk_write<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                           tcnt, toff, bbase, meta, d_vals, d_idx,
                                                                           tflags, ncov);

@@ -652,11 +652,14 @@ struct Stager {
 // k_tk5_write).  A segment that overflows sets seg.ovf: the top-k then counts
 // and writes from the input (exact, slower).
 struct TkSeg {
-    int32_t *vals;  // nwaves * cap raw keys
-    uint8_t *pos;   // their positions in their wave-rows
-    uint32_t cap;   // entries per segment
-    uint32_t *ovf;  // set to 1 when any segment overflows
+    int32_t *vals;     // nwaves * cap raw keys
+    uint8_t *pos;      // their positions in their wave-rows
+    uint32_t cap;      // entries per segment
+    uint32_t *ovf;     // set to 1 when any segment overflows
+    uint32_t *wstart;  // nwaves * nwin: entries a wave staged before each window of TK5_WIN_TILES tiles
+    uint32_t nwin;     // windows per wave
 };
+constexpr int TK5_WIN_TILES = 8;  // a window of the staged top-k kernels: 8 tiles = 64 wave-rows a wave
 
 struct OrdStager {
     static constexpr uint32_t CAP = ((uint32_t)WREG * 4 / 5) & ~63u;  // keys; CAP position bytes follow
@@ -707,33 +710,58 @@ struct OrdStager {
     }
 
     // One wave-row slot: this lane's 4 consecutive keys q (positions p0 .. p0 + 3
-    // of the wave-row), f = the keys to stage (bit j: key j).  Appends them in
-    // index order; returns the wave's count (wave-uniform).
-    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t f, uint32_t p0) {
-        const uint32_t c = (uint32_t)__popc(f);
-        if (__builtin_amdgcn_ballot_w64(c != 0) == 0) return 0u;  // wave-uniform
-        const uint32_t incl = wave_incl_scan32(c);
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+    // of the wave-row; key j valid iff bit j of valid4); stages the keys on the
+    // kept side of the far edge (x <= hi for TF 5, x >= lo for TF 6) in index
+    // order.  Returns the wave's count (wave-uniform).  When no lane stages two
+    // of its 4 keys (the usual case: ~1-2 % of the keys are staged), a key's
+    // slot is the fill plus mbcnt of the OR'ed ballots and the key is picked by
+    // selects on the ballots; otherwise a wave scan of the per-lane counts.
+    template <int TF>
+    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t valid4, uint32_t p0) {
+        auto f1 = [&](uint32_t x, int j) {
+            return ((valid4 >> j) & 1u) != 0u && (TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo);
+        };
+        const bool c0 = f1(q.x, 0), c1 = f1(q.y, 1), c2 = f1(q.z, 2), c3 = f1(q.w, 3);
+        const unsigned long long b0 = __builtin_amdgcn_ballot_w64(c0), b1 = __builtin_amdgcn_ballot_w64(c1),
+                                 b2 = __builtin_amdgcn_ballot_w64(c2), b3 = __builtin_amdgcn_ballot_w64(c3);
+        const unsigned long long any = b0 | b1 | b2 | b3;
+        if (any == 0) return 0u;  // wave-uniform
+        const uint32_t total = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+#ifdef KTH_DIAG_TK5_NOSTAGE  // diagnostic builds only (wrong top-k results): cost of the staging
+        return total;
+#endif
         if (wfill + total > CAP) flush();
-        uint32_t at = wfill + incl - c;
         uint8_t *pb = reinterpret_cast<uint8_t *>(reg + CAP);
-        if (f & 1u) { reg[at] = q.x; pb[at] = (uint8_t)p0; ++at; }
-        if (f & 2u) { reg[at] = q.y; pb[at] = (uint8_t)(p0 + 1); ++at; }
-        if (f & 4u) { reg[at] = q.z; pb[at] = (uint8_t)(p0 + 2); ++at; }
-        if (f & 8u) { reg[at] = q.w; pb[at] = (uint8_t)(p0 + 3); }
+        const unsigned long long coll = (b0 & b1) | ((b0 | b1) & b2) | ((b0 | b1 | b2) & b3);
+        if (coll == 0) {  // wave-uniform
+            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, wfill));
+            // (selects in asm: as ?: the compiler may index the keys through scratch)
+            uint32_t val = q.x, j;
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.y), "s"(b1));
+            asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(j) : "s"(b1));
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.z), "s"(b2));
+            asm("v_cndmask_b32_e64 %0, %1, 2, %2" : "=v"(j) : "v"(j), "s"(b2));
+            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.w), "s"(b3));
+            asm("v_cndmask_b32_e64 %0, %1, 3, %2" : "=v"(j) : "v"(j), "s"(b3));
+            if (c0 || c1 || c2 || c3) {
+                reg[at] = val;
+                pb[at] = (uint8_t)(p0 + j);
+            }
+        } else {
+            const uint32_t c = (c0 ? 1u : 0u) + (c1 ? 1u : 0u) + (c2 ? 1u : 0u) + (c3 ? 1u : 0u);
+            const uint32_t incl = wave_incl_scan32(c);
+            uint32_t at = wfill + incl - c;
+            if (c0) { reg[at] = q.x; pb[at] = (uint8_t)p0; ++at; }
+            if (c1) { reg[at] = q.y; pb[at] = (uint8_t)(p0 + 1); ++at; }
+            if (c2) { reg[at] = q.z; pb[at] = (uint8_t)(p0 + 2); ++at; }
+            if (c3) { reg[at] = q.w; pb[at] = (uint8_t)(p0 + 3); }
+        }
         wfill += total;
         return total;
     }
 };
 static_assert(OrdStager::CAP + OrdStager::CAP / 4 <= (uint32_t)WREG && OrdStager::CAP >= 4 * WAVE,
               "OrdStager region: keys + position bytes in one wave's region, >= one wave-row");
-
-// the 4 keys of q a TF 5 / 6 pass stages (x <= hi / x >= lo), as bits
-template <int TF>
-__device__ __forceinline__ uint32_t ord_flags(const uint4 &q, int32_t slo, int32_t shi, uint32_t valid4 = 0xFu) {
-    auto f1 = [&](uint32_t x) { return TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo; };
-    return ((f1(q.x) ? 1u : 0u) | (f1(q.y) ? 2u : 0u) | (f1(q.z) ? 4u : 0u) | (f1(q.w) ? 8u : 0u)) & valid4;
-}
 
 // Count and stage K keys of this lane (key j valid iff bit j of `valid`).  The
 // keys are the raw int32 words: signed compares against the signed window
@@ -786,11 +814,22 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 // 3 / 4 (k smallest / largest, k > n / 1024): per full tile, row u and wave,
 // one word #beyond (#<lo for 3, #>hi for 4; <= 256 keys a wave-row), or'ed
 // with TK_RECOUNT when the wave-tile holds a key equal to lo or hi, at
-// tflags[4 + (row * 4 + wave)], row = tile * U + u; and every candidate's row
+// tflags[row_word(row, wave)], row = tile * U + u; and every candidate's row
 // in cand_rows.  With the candidates these give every unmarked row's #better /
 // #equal for any k-th inside the window, so the top-k re-reads only marked
 // rows to count (k_topk_count<.., META>).
 constexpr uint32_t TK_RECOUNT = 1u << 31;
+// Where k_main<TF >= 3> keeps wave w's word of row r (tflags index): wave w
+// of tile t (rows 8t .. 8t + 7) stores its 8 row words as one contiguous,
+// 32-byte aligned sector, so a row's four words are 8 apart.  (Row-major --
+// a row's four words adjacent -- made every wave's store 8 scattered dwords
+// of a 128-byte line that three other waves complete later: partial-line
+// writes, which cost the pass 60-80 us at 2^30.)  Words start after an 8-word
+// header (lo, hi, valid, segment overflow; tflags is 64-byte aligned).
+constexpr u64 TF_W0 = 8;
+__host__ __device__ __forceinline__ u64 row_word(u64 r, uint32_t w) {
+    return TF_W0 + ((r / MAIN_UNROLL) * (BLK / WAVE) + w) * MAIN_UNROLL + r % MAIN_UNROLL;
+}
 static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot in a byte");
 static_assert(BLK / WAVE == 4, "k_main<TF> stores one flag byte per wave, four per tile (tk_row_flagged's mask)");
 template <int TF>
@@ -824,11 +863,17 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     // early finishers' bandwidth goes to the rest.  DESIGN.md.)
     auto load_tile = [&](uint4 (&x)[U], u64 t) {
         const uint4 *src = v + t * tile + threadIdx.x;
+        // Two loads, wait for the first, then the other U-2: the compiler's
+        // own order for k_main<0>.  Sending all U first (a sched_barrier after
+        // the loads, and the top-k variants' own schedule) made the pass slower:
+        // k_main<0> 640 -> 685 us, k_main<5> ~750 vs 640 at 2^30.
+        x[0] = load_nt(src);
+        x[1] = load_nt(src + BLK);
+#ifndef KTH_MAIN_NOWAIT1
+        if constexpr (TF != 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+#endif
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = load_nt(src + u * BLK);
-        // (The compiler issues 2 loads, waits for the first, then issues the
-        // other U-2.  A sched_barrier here that sends all U first measured
-        // slower: k_main 640 -> 685 us.)
+        for (int u = 2; u < U; ++u) x[u] = load_nt(src + u * BLK);
     };
     // (Issuing the first tile's loads before the advance made the pass slower,
     // 656 vs 642 us: the advance's histogram loads then wait behind them.)
@@ -851,6 +896,10 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
     // TF 5 / 6: the counts of 4 keys (as scan_keys) and their ordered staging
     auto ord_keys = [&](const uint4 &q, uint32_t valid4, uint32_t p0) -> uint32_t {
+#ifdef KTH_DIAG_TK5_NOROW  // diagnostic builds only (wrong results): the pass without the staging compares
+        clt += q.x < (uint32_t)slo;
+        return 0u;
+#endif
         const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -860,7 +909,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             ceqlo += (ok & (x == slo)) ? 1u : 0u;
             ceqhi += (ok & (x == shi)) ? 1u : 0u;
         }
-        return os.row(q, ord_flags<TF>(q, slo, shi, valid4), p0);
+        return os.template row<TF>(q, valid4, p0);
     };
 
     // a tile is consumed in groups of 4 * MAIN_SUB keys
@@ -945,19 +994,21 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 const uint32_t q = lane < 4 ? 0u : 2u, sh = 8 * (lane & 3);
                 const uint32_t word = ((rx[q] >> sh) & 0xFFu) + ((rx[q + 1] >> sh) & 0xFFu);
                 pend_word = word | mark;
-                pend_at = 4 + ((t * U + lane) * (BLK / WAVE) + wid);
+                pend_at = row_word(t * U + lane, (uint32_t)wid);
             }
             __builtin_amdgcn_wave_barrier();
         }
     };
-    // every load of a tile issued before any use
+    uint32_t tiles_done = 0;  // TF 5 / 6: this workgroup's tiles so far (its windows' starts)
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
         const uint32_t e0 = ceqlo + ceqhi, c0 = clt;
         load_tile(x, t);
+#ifndef KTH_DIAG_NOPEND  // diagnostic builds only (wrong top-k results): cost of the row-word stores
         if constexpr (TF >= 3)
             if (pend_at != ~0ull) tflags[pend_at] = pend_word;  // the previous tile's words (lanes 0..U-1)
+#endif
         if constexpr (ORD) {
             // row u: this lane's keys 4 * lane .. + 3 of the wave's 256 (its wave-row);
             // lane u keeps row u's staged count for the row words
@@ -969,8 +1020,14 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             }
             if (lane < U) {
                 pend_word = rw;
-                pend_at = 4 + ((t * U + lane) * (BLK / WAVE) + wid);
+                pend_at = row_word(t * U + lane, (uint32_t)wid);
             }
+            // the entries staged before the next window (its first tile), so the
+            // staged top-k kernels take the windows independently
+            ++tiles_done;
+            if (tiles_done % TK5_WIN_TILES == 0 && tiles_done / TK5_WIN_TILES < seg.nwin && lane == 0)
+                seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + tiles_done / TK5_WIN_TILES] =
+                    os.seg_fill + os.wfill;
         } else {
             scan_tile(x, t, ra);
             flag_tile(x, t, ra, e0, c0);

@@ -94,9 +94,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
         bool act = tl < ntiles;
         if (staged_ok && tl < ncov) act = false;  // counted by k_tk5_count
         if (act && meta_ok && tl < ncov) {
-            const uint4 w = reinterpret_cast<const uint4 *>(fw)[tl];
-            if (((w.x | w.y | w.z | w.w) & TK_RECOUNT) == 0u) {
-                tcnt[tl] += w.x + w.y + w.z + w.w;  // k_topk_cands ran first: add to the candidates' share
+            const uint32_t w0 = tflags[row_word(tl, 0)], w1 = tflags[row_word(tl, 1)], w2 = tflags[row_word(tl, 2)],
+                           w3 = tflags[row_word(tl, 3)];
+            if (((w0 | w1 | w2 | w3) & TK_RECOUNT) == 0u) {
+                tcnt[tl] += w0 + w1 + w2 + w3;  // k_topk_cands ran first: add to the candidates' share
                 act = false;
             }
         }
@@ -369,9 +370,52 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
 // whose entries are the wave's wave-rows' staged keys back to back in that
 // order (row words: counts).  Lane l takes one wave-row of each window of 64.
 
+// The entries of one wave-row, e in [0, c), four loads in flight per lane
+// (a rolled per-entry loop waited one memory round trip per entry); with sp,
+// their positions are loaded beside them (f(x, p)).
+template <typename F>
+__device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
+                                            uint32_t c, F &&f) {
+    for (uint32_t e0 = 0; e0 < c; e0 += 4) {
+        int32_t x[4];
+        uint8_t p[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            x[q] = e0 + q < c ? sv[e0 + q] : 0;
+            if (sp) p[q] = e0 + q < c ? sp[e0 + q] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (e0 + q < c) f(x[q], p[q]);
+    }
+}
+
+// The staged kernels' split: gridDim.x = G * S workgroups; workgroup
+// (b, part) takes part `part` of the windows of k_main's workgroup b (its
+// waves' segments), each window starting at the entry offsets k_main<5/6>
+// recorded (seg.wstart), so no window waits for the one before it.
+struct Tk5Part {
+    u64 b, G, m, w_lo, w_hi;  // k_main workgroup, its grid, its wave-rows, windows [w_lo, w_hi)
+};
+__device__ __forceinline__ Tk5Part tk5_part(u64 nfull, u64 G) {
+    Tk5Part t;
+    t.G = G;
+    t.b = blockIdx.x % G;
+    const u64 part = blockIdx.x / G, S = gridDim.x / G;
+    t.m = (nfull > t.b ? (nfull - 1 - t.b) / G + 1 : 0) * MAIN_UNROLL;
+    const u64 nw = (t.m + WAVE - 1) / WAVE;
+    t.w_lo = part * nw / S;
+    t.w_hi = (part + 1) * nw / S;
+    return t;
+}
+__device__ __forceinline__ uint32_t tk5_wstart(const uint32_t *wstart, uint32_t nwin, u64 b, int w, u64 win) {
+    return win == 0 ? 0u : wstart[(b * (TK_BLOCK / WAVE) + (u64)w) * nwin + win];
+}
+
 // Per wave-row: #better | #equal << 16 -> wcnt; per row (the 4 wave-rows of
 // its 4 waves, summed through LDS) -> tcnt.  Entries are read, the input is not.
 __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restrict__ segv, u64 seg_cap,
+                                                        const uint32_t *__restrict__ wstart, uint32_t nwin, u64 G,
                                                         const uint32_t *__restrict__ tflags, u64 nfull,
                                                         const int32_t *__restrict__ d_v, uint32_t flip,
                                                         uint32_t *__restrict__ wcnt, uint32_t *__restrict__ tcnt) {
@@ -379,24 +423,19 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
     if (!tk5_ok(tflags, d_v)) return;  // grid-uniform
     const int32_t v = d_v[0];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-    const u64 b = blockIdx.x, G = gridDim.x;
-    const u64 m = (nfull > b ? (nfull - 1 - b) / G + 1 : 0) * MAIN_UNROLL;  // this wave's wave-rows
-    const int32_t *sv = segv + (b * (TK_BLOCK / WAVE) + w) * seg_cap;
-    uint32_t carry = 0;
-    for (u64 j0 = 0; j0 < m; j0 += WAVE) {  // same trip count in the 4 waves
-        const u64 j = j0 + lane;
-        const bool valid = j < m;
-        const u64 r = (b + (j / MAIN_UNROLL) * G) * MAIN_UNROLL + j % MAIN_UNROLL;
-        const uint32_t c = valid ? tflags[4 + r * (TK_BLOCK / WAVE) + w] : 0u;
-        const uint32_t incl = wave_incl_scan32(c);
-        const uint32_t start = carry + incl - c;
-        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+    const Tk5Part P = tk5_part(nfull, G);
+    const int32_t *sv = segv + (P.b * (TK_BLOCK / WAVE) + w) * seg_cap;
+    for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
+        const u64 j = win * WAVE + lane;
+        const bool valid = j < P.m;
+        const u64 r = (P.b + (j / MAIN_UNROLL) * P.G) * MAIN_UNROLL + j % MAIN_UNROLL;
+        const uint32_t c = valid ? tflags[row_word(r, (uint32_t)w)] : 0u;
+        const uint32_t start = tk5_wstart(wstart, nwin, P.b, w, win) + wave_incl_scan32(c) - c;
         uint32_t nb = 0, ne = 0;
-        for (uint32_t e = 0; e < c; ++e) {
-            const int32_t x = sv[start + e];
+        tk5_entries(sv + start, nullptr, c, [&](int32_t x, uint8_t) {
             nb += (flip == 0u ? x < v : x > v) ? 1u : 0u;
             ne += x == v ? 1u : 0u;
-        }
+        });
         const uint32_t word = nb | ne << 16;
         if (valid) wcnt[r * (TK_BLOCK / WAVE) + w] = word;
         part[w][lane] = word;
@@ -410,57 +449,132 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
 // #better before it + min(#equal before it, need), as in k_topk_write; the
 // wave-row's bases are its row's (toff, bbase) plus the earlier waves' counts
 // in the row (wcnt), and the entries are in index order within the wave-row.
+// The workgroup's 4 waves take the same 64 rows at a time (8 of k_main's
+// 8-row tiles; wave w: quarter w of each row).  A tile's 8192 keys are
+// consecutive, so its output is one contiguous range: the kept entries are
+// placed in LDS at their offsets in their tile's range and written out
+// coalesced (lane-scattered stores wrote ~64 cache lines an instruction:
+// 300 us at k = 2^24).  A window whose output exceeds the stage is written
+// directly.  The next window's row records are loaded while this one is
+// placed and copied (the loop is a chain of dependent loads and barriers).
+constexpr int TK5_STAGE = 4096;  // output entries a workgroup stages (24 KiB of LDS: k_main's grid stays resident)
+struct Tk5Rec {                  // one lane's row records of a window
+    uint32_t c, tc;              // the wave-row's entries; the row's count word
+    u64 off, b0, b1;             // toff[r], bbase[2 blk], bbase[2 blk + 1]
+    uint4 wc;                    // the row's four wave-row words
+};
+__device__ __forceinline__ Tk5Rec tk5_rec(const uint32_t *__restrict__ tflags, const uint32_t *__restrict__ wcnt,
+                                          const uint32_t *__restrict__ tcnt, const u64 *__restrict__ toff,
+                                          const u64 *__restrict__ bbase, u64 r, bool valid, int w) {
+    Tk5Rec x{0u, 0u, 0ull, 0ull, 0ull, make_uint4(0u, 0u, 0u, 0u)};
+    if (valid) {
+        const u64 blk = r / TK_TILES_PER_BLOCK;
+        x.c = tflags[row_word(r, (uint32_t)w)];
+        x.tc = tcnt[r];
+        x.off = toff[r];
+        x.b0 = bbase[2 * blk];
+        x.b1 = bbase[2 * blk + 1];
+        x.wc = *reinterpret_cast<const uint4 *>(wcnt + r * (TK_BLOCK / WAVE));
+    }
+    return x;
+}
 __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restrict__ segv,
                                                         const uint8_t *__restrict__ segp, u64 seg_cap,
+                                                        const uint32_t *__restrict__ wstart, uint32_t nwin, u64 G,
                                                         const uint32_t *__restrict__ tflags, u64 nfull,
                                                         const int32_t *__restrict__ d_v, uint32_t flip,
                                                         const uint32_t *__restrict__ wcnt,
+                                                        const uint32_t *__restrict__ tcnt,
                                                         const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
                                                         const u64 *__restrict__ meta, int32_t *__restrict__ vals,
                                                         int64_t *__restrict__ idx) {
+    __shared__ int32_t s_val[TK5_STAGE];
+    __shared__ uint16_t s_loc[TK5_STAGE];  // key index within its tile: u << 10 | w << 8 | position
+    __shared__ u64 s_lo[8];                // tile i of the window: its first output slot
+    __shared__ uint32_t s_off[9];          // and its first stage entry (s_off[8]: the window's total)
     if (!tk5_ok(tflags, d_v) || meta[1]) return;  // grid-uniform
     const u64 need = meta[0];
     const int32_t v = d_v[0];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-    const u64 b = blockIdx.x, G = gridDim.x;
-    const u64 m = (nfull > b ? (nfull - 1 - b) / G + 1 : 0) * MAIN_UNROLL;
+    const Tk5Part P = tk5_part(nfull, G);
+    const u64 b = P.b, m = P.m;  // m: a multiple of 8, whole tiles
     const u64 sbase = (b * (TK_BLOCK / WAVE) + w) * seg_cap;
-    uint32_t carry = 0;
-    for (u64 j0 = 0; j0 < m; j0 += WAVE) {
-        const u64 j = j0 + lane;
+    static_assert(MAIN_UNROLL == 8 && WAVE / MAIN_UNROLL == 8 && TK5_WIN_TILES * MAIN_UNROLL == WAVE,
+                  "a window of 64 rows is 8 tiles");
+    auto row_of = [&](u64 j) { return (b + (j / MAIN_UNROLL) * G) * MAIN_UNROLL + j % MAIN_UNROLL; };
+    auto from = [](u64 x, int l) {  // x of lane l (per-lane l: bpermute)
+        return ((u64)(uint32_t)__shfl((int)(uint32_t)(x >> 32), l, WAVE) << 32) |
+               (uint32_t)__shfl((int)(uint32_t)x, l, WAVE);
+    };
+    Tk5Rec nx = tk5_rec(tflags, wcnt, tcnt, toff, bbase, row_of(P.w_lo * WAVE + lane), P.w_lo * WAVE + lane < m, w);
+    for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
+        const u64 j0 = win * WAVE, j = j0 + lane;
         const bool valid = j < m;
-        const u64 r = (b + (j / MAIN_UNROLL) * G) * MAIN_UNROLL + j % MAIN_UNROLL;
-        const uint32_t c = valid ? tflags[4 + r * (TK_BLOCK / WAVE) + w] : 0u;
-        const uint32_t incl = wave_incl_scan32(c);
-        const uint32_t start = carry + incl - c;
-        carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
-        if (c == 0) continue;
-        const u64 off = toff[r], blk = r / TK_TILES_PER_BLOCK;
-        u64 bb = bbase[2 * blk] + (off & 0xFFFFFFFFull), be = bbase[2 * blk + 1] + (off >> 32);
-        const uint4 wc = *reinterpret_cast<const uint4 *>(wcnt + r * (TK_BLOCK / WAVE));
-        const uint32_t wcs[4] = {wc.x, wc.y, wc.z, wc.w};
+        const u64 r = row_of(j);
+        const Tk5Rec cur = nx;
+        if (win + 1 < P.w_hi) nx = tk5_rec(tflags, wcnt, tcnt, toff, bbase, row_of(j + WAVE), j + WAVE < m, w);
+        const uint32_t c = cur.c;
+        const uint32_t start = tk5_wstart(wstart, nwin, b, w, win) + wave_incl_scan32(c) - c;
+        // this row's bases, and this wave-row's (after the earlier quarters' counts)
+        const u64 rb = cur.b0 + (cur.off & 0xFFFFFFFFull), re = cur.b1 + (cur.off >> 32);
+        u64 bb = rb, be = re;
+        const uint32_t wcs[4] = {cur.wc.x, cur.wc.y, cur.wc.z, cur.wc.w};
 #pragma unroll
         for (int q = 0; q < TK_BLOCK / WAVE; ++q)
             if (q < w) {
                 bb += wcs[q] & 0xFFFFu;
                 be += wcs[q] >> 16;
             }
+        // each tile's output range (its first row's start to its last row's
+        // end); every wave computes the same table, wave 0 publishes it
+        const u64 lo = rb + (re < need ? re : need);
+        const u64 e2 = re + tk_equal_of(cur.tc);
+        const u64 hi = rb + tk_better_of(cur.tc) + (e2 < need ? e2 : need);
+        const u64 tlo = from(lo, lane & ~7), thi = from(hi, lane | 7);
+        const uint32_t len = (lane & 7) == 0 && valid ? (uint32_t)(thi - tlo) : 0u;
+        const uint32_t li = wave_incl_scan32(len);  // lanes 0, 8, .., 56 hold the tiles' lengths
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)li, WAVE - 1);
+        const uint32_t toff_s = (uint32_t)__shfl((int)(li - len), lane & ~7, WAVE);  // this lane's tile's first entry
+        if (w == 0 && (lane & 7) == 0) {
+            s_lo[lane >> 3] = tlo;
+            s_off[lane >> 3] = li - len;
+        }
+        if (w == 0 && lane == 0) s_off[8] = total;
+        const bool staged = total <= (uint32_t)TK5_STAGE;  // block-uniform
+        const uint16_t loc0 = (uint16_t)((lane & 7) << 10 | w << 8);
         const u64 i0 = r * TK_TILE + (u64)w * (TK_TILE / (TK_BLOCK / WAVE));  // the wave-row's first key
-        for (uint32_t e = 0; e < c; ++e) {
-            const int32_t x = segv[sbase + start + e];
-            u64 pos = ~0ull;
-            if (flip == 0u ? x < v : x > v) {
-                pos = bb + (be < need ? be : need);
-                ++bb;
-            } else if (x == v) {
-                if (be < need) pos = bb + be;
-                ++be;
+        tk5_entries(segv + sbase + start, segp + sbase + start, c, [&](int32_t x, uint8_t p) {
+            // (selects, not branches: with ++bb / ++be in branches the compiler
+            // kept the pair in scratch and incremented it through a pointer)
+            const bool isb = flip == 0u ? x < v : x > v, ise = x == v;
+            const bool keep = isb || (ise && be < need);
+            const u64 pos = bb + (be < need ? be : need);  // == bb + be for a kept equal entry
+            bb += isb ? 1u : 0u;
+            be += ise ? 1u : 0u;
+            if (keep) {
+                if (staged) {
+                    const uint32_t s = toff_s + (uint32_t)(pos - tlo);
+                    s_val[s] = x;
+                    s_loc[s] = (uint16_t)(loc0 | p);
+                } else {
+                    if (vals) vals[pos] = x;
+                    if (idx) idx[pos] = (int64_t)(i0 + p);
+                }
             }
-            if (pos != ~0ull) {
-                if (vals) vals[pos] = x;
-                if (idx) idx[pos] = (int64_t)(i0 + segp[sbase + start + e]);
+        });
+        if (staged) {  // coalesced copy-out, tile by tile
+            __syncthreads();
+            const u64 tile0 = (b + (j0 / MAIN_UNROLL) * G) * MAIN_UNROLL * TK_TILE;  // the window's first tile's first key
+            for (uint32_t s = threadIdx.x; s < total; s += TK_BLOCK) {
+                int i = 0;
+#pragma unroll
+                for (int q = 1; q < 8; ++q) i += s >= s_off[q] ? 1 : 0;
+                const u64 gp = s_lo[i] + (s - s_off[i]);
+                if (vals) vals[gp] = s_val[s];
+                if (idx) idx[gp] = (int64_t)(tile0 + (u64)i * G * MAIN_UNROLL * TK_TILE + s_loc[s]);
             }
         }
+        __syncthreads();  // the stage and the tile table are reused by the next window
     }
 }
 

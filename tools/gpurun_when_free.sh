@@ -1,0 +1,16 @@
+#!/bin/bash
+# Submit one gpurun call; when gpurun reports that NOTHING ran (exit 3: no box
+# or slot free, box lost while being prepared -- nothing charged), submit the
+# same call again after a pause, at most 6 times.  Any other exit (the command
+# ran, passed or failed) ends it: a failing GPU run is never repeated.
+# usage: tools/gpurun_when_free.sh LOG TIMEOUT 'command'
+log=$1; to=$2; cmd=$3
+for attempt in 1 2 3 4 5 6; do
+  /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
+  rc=$?
+  [ $rc -eq 3 ] || break
+  echo "attempt $attempt: no box (rc 3), waiting" >> "$log.tries"
+  sleep 120
+done
+echo "rc=$rc" >> "$log"
+exit $rc

@@ -14,8 +14,9 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
         print(f"{k:40s} calls {len(v):4d} avg {sum(v) / len(v):9.1f} us  min {min(v):9.1f}")
 ks = [r for r in rows if "kth::" in r["Kernel_Name"]]
 starts = [i for i, r in enumerate(ks) if "k_gather" in r["Kernel_Name"] or "k_head" in r["Kernel_Name"]]
-if starts:
-    seq = ks[starts[-1]:starts[-1] + (int(sys.argv[2]) if len(sys.argv) > 2 else 8)]
+ntl = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+if starts and ntl > 0:
+    seq = ks[starts[-1]:starts[-1] + ntl]
     t0 = int(seq[0]["Start_Timestamp"])
     for r in seq:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
