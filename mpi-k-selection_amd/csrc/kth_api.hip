@@ -983,13 +983,14 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
                                                              : 0;
     const u64 ncov = tf >= 3 ? nfull * kth::MAIN_UNROLL : 0;  // tiles = k_main rows (head == 0)
     // tflags: the header and TF 1 / 2's flag bytes after 4 words, TF >= 3's
-    // row words after TF_W0 (kth::row_word); 64-byte aligned, so that a wave's
-    // 8 row words fill one 32-byte sector
-    const u64 fwords = tf >= 3 ? kth::TF_W0 + ncov * (kth::BLK / kth::WAVE) : 4 + nfull;
+    // row words after TF_W0 in per-wave segments (kth::rw_index); 256-byte
+    // aligned, so that a wave's group of 64 words fills one line
+    const kth::RowWords rwl{(u64)c->main_grid[tf], kth::rw_seg_words(nfull, (u64)c->main_grid[tf])};
+    const u64 fwords = tf >= 3 ? kth::TF_W0 + rwl.G * (kth::BLK / kth::WAVE) * rwl.seg : 4 + nfull;
     const u64 fw64 = (fwords + 1) / 2, before = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2;
-    const u64 words = before + fw64 + 8;
+    const u64 words = before + fw64 + 32;
     KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
-    const u64 foff = (before + 7) & ~7ull;  // + fw64 <= words
+    const u64 foff = (before + 31) & ~31ull;  // + fw64 <= words
     uint32_t *tflags = reinterpret_cast<uint32_t *>(c->topk + foff);
     HIP_TRY(hipMemsetAsync(tflags, 0, 16, c->stream));  // window header: not valid until k_main<TF> runs
     if (tf == 3 || tf == 4) {
@@ -1034,7 +1035,7 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         kth::k_topk_cands<<<c->num_cu * 8, kth::TK_BLOCK, 0, c->stream>>>(
             c->cand, c->cand_rows, cand_count(c), c->cand_cap / 4, c->d_status, flip, tcnt, tflags, sel_st);
         kth::k_topk_count<true, 1><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
-                                                                          tcnt, tflags, head, nfull, sel_st, ncov);
+                                                                          tcnt, tflags, head, nfull, sel_st, ncov, rwl);
     } else if (aligned) {
         kth::k_topk_count<true, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                            tcnt, tflags, head, nfull, sel_st, 0);

@@ -814,21 +814,34 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 // 3 / 4 (k smallest / largest, k > n / 1024): per full tile, row u and wave,
 // one word #beyond (#<lo for 3, #>hi for 4; <= 256 keys a wave-row), or'ed
 // with TK_RECOUNT when the wave-tile holds a key equal to lo or hi, at
-// tflags[row_word(row, wave)], row = tile * U + u; and every candidate's row
+// tflags[rw_index(row, wave)], row = tile * U + u; and every candidate's row
 // in cand_rows.  With the candidates these give every unmarked row's #better /
 // #equal for any k-th inside the window, so the top-k re-reads only marked
 // rows to count (k_topk_count<.., META>).
 constexpr uint32_t TK_RECOUNT = 1u << 31;
-// Where k_main<TF >= 3> keeps wave w's word of row r (tflags index): wave w
-// of tile t (rows 8t .. 8t + 7) stores its 8 row words as one contiguous,
-// 32-byte aligned sector, so a row's four words are 8 apart.  (Row-major --
-// a row's four words adjacent -- made every wave's store 8 scattered dwords
-// of a 128-byte line that three other waves complete later: partial-line
-// writes, which cost the pass 60-80 us at 2^30.)  Words start after an 8-word
-// header (lo, hi, valid, segment overflow; tflags is 64-byte aligned).
-constexpr u64 TF_W0 = 8;
-__host__ __device__ __forceinline__ u64 row_word(u64 r, uint32_t w) {
-    return TF_W0 + ((r / MAIN_UNROLL) * (BLK / WAVE) + w) * MAIN_UNROLL + r % MAIN_UNROLL;
+// Where k_main<TF >= 3> keeps wave w's word of row r: in wave-major segments
+// (one per k_main wave, `seg` words: 8 per tile the workgroup streams,
+// rounded up to 64), tile i of the workgroup at word 8 i.  A wave collects the
+// words of 128 tiles in RW_REGS = 16 registers of its 64 lanes and stores
+// them as 16 256-byte lines every 128th tile (at 2^30: once, after the loop).  Stores count in vmcnt in issue order, so a
+// store in the loop makes the next tile's first load wait for the store's
+// acknowledgement, which under the streaming reads takes microseconds: a
+// store per tile cost the pass ~80 us at 2^30, one per 8 tiles ~60 us, one
+// per 64 tiles ~30 us.
+// Words start after a 64-word header (lo, hi, valid, segment overflow);
+// tflags is 256-byte aligned.
+constexpr u64 TF_W0 = 64;
+constexpr int RW_REGS = 16;  // registers of row words a k_main<TF >= 3> wave holds (8 tiles each)
+struct RowWords {
+    u64 G;    // k_main's grid (workgroups)
+    u64 seg;  // words per wave segment
+};
+__host__ __device__ __forceinline__ u64 rw_seg_words(u64 nfull, u64 G) {
+    return ((nfull + G - 1) / G * MAIN_UNROLL + 63) / 64 * 64;
+}
+__host__ __device__ __forceinline__ u64 rw_index(const RowWords &L, u64 r, uint32_t w) {
+    const u64 t = r / MAIN_UNROLL;
+    return TF_W0 + ((t % L.G) * (BLK / WAVE) + w) * L.seg + (t / L.G) * MAIN_UNROLL + r % MAIN_UNROLL;
 }
 static_assert(MAIN_UNROLL <= 8, "k_main<TF> keeps one row bit per 16-B load slot in a byte");
 static_assert(BLK / WAVE == 4, "k_main<TF> stores one flag byte per wave, four per tile (tk_row_flagged's mask)");
@@ -931,12 +944,14 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         }
     };
     // (e0: this lane's ceqlo + ceqhi before the tile; a change = a key on an edge)
-    // TF 3 / 4: a wave-tile's row words are stored one tile later, after the
-    // next tile's loads are issued (stored at once, the store's data register
-    // was reused by the next tile's load addresses and the compiler made the
-    // loads wait for the store: +70 us a pass); pend_at = word index (~0: none).
-    u64 pend_at = ~0ull;
-    uint32_t pend_word = 0;
+    // TF >= 3: lanes 0..U-1 leave the tile's row words in tile_word; lane
+    // 8 (i % 8) + u of grp collects row u of the workgroup's tile i, and the
+    // 64 lanes store every 8th tile (rw_index)
+    uint32_t tile_word = 0, grp[RW_REGS], wsr = 0;
+#pragma unroll
+    for (int q = 0; q < RW_REGS; ++q) grp[q] = 0u;
+    const u64 seg_words = rw_seg_words(nfull, gridDim.x);
+    uint32_t *const wseg = tflags + TF_W0 + ((u64)blockIdx.x * (BLK / WAVE) + wid) * seg_words;
     auto flag_tile = [&](const uint4 (&x)[U], u64 t, RowAcc &ra, uint32_t e0, uint32_t c0) {
         if constexpr (TF == 1 || TF == 2) {
             // bit u of the wave's byte: some key of row u (the tile's u-th run of
@@ -993,22 +1008,18 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             if (lane < U) {
                 const uint32_t q = lane < 4 ? 0u : 2u, sh = 8 * (lane & 3);
                 const uint32_t word = ((rx[q] >> sh) & 0xFFu) + ((rx[q + 1] >> sh) & 0xFFu);
-                pend_word = word | mark;
-                pend_at = row_word(t * U + lane, (uint32_t)wid);
+                tile_word = word | mark;
             }
             __builtin_amdgcn_wave_barrier();
         }
     };
-    uint32_t tiles_done = 0;  // TF 5 / 6: this workgroup's tiles so far (its windows' starts)
+    static_assert(TK5_WIN_TILES * U == WAVE, "a group of row words is one window of the staged kernels");
+    uint32_t tiles_done = 0;  // TF >= 3: this workgroup's tiles so far
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
         const uint32_t e0 = ceqlo + ceqhi, c0 = clt;
         load_tile(x, t);
-#ifndef KTH_DIAG_NOPEND  // diagnostic builds only (wrong top-k results): cost of the row-word stores
-        if constexpr (TF >= 3)
-            if (pend_at != ~0ull) tflags[pend_at] = pend_word;  // the previous tile's words (lanes 0..U-1)
-#endif
         if constexpr (ORD) {
             // row u: this lane's keys 4 * lane .. + 3 of the wave's 256 (its wave-row);
             // lane u keeps row u's staged count for the row words
@@ -1018,23 +1029,51 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 const uint32_t tot = ord_keys(x[u], 0xFu, 4u * (uint32_t)lane);
                 rw = lane == u ? tot : rw;
             }
-            if (lane < U) {
-                pend_word = rw;
-                pend_at = row_word(t * U + lane, (uint32_t)wid);
-            }
-            // the entries staged before the next window (its first tile), so the
-            // staged top-k kernels take the windows independently
-            ++tiles_done;
-            if (tiles_done % TK5_WIN_TILES == 0 && tiles_done / TK5_WIN_TILES < seg.nwin && lane == 0)
-                seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + tiles_done / TK5_WIN_TILES] =
-                    os.seg_fill + os.wfill;
+            tile_word = rw;
         } else {
             scan_tile(x, t, ra);
             flag_tile(x, t, ra, e0, c0);
         }
+        if constexpr (TF >= 3) {
+            // lane 8 (i % 8) + u of grp[(i / 8) % RW_REGS] <- row u of tile i
+            const uint32_t v = (uint32_t)__shfl((int)tile_word, lane & (U - 1), WAVE);
+            const bool mine = (uint32_t)(lane / U) == tiles_done % TK5_WIN_TILES;
+            const uint32_t gi = (tiles_done / TK5_WIN_TILES) % RW_REGS;
+#pragma unroll
+            for (int q = 0; q < RW_REGS; ++q) grp[q] = mine && gi == (uint32_t)q ? v : grp[q];
+            ++tiles_done;
+#ifndef KTH_DIAG_NOPEND  // diagnostic builds only (wrong top-k results): cost of the row-word stores
+            if (tiles_done % (RW_REGS * TK5_WIN_TILES) == 0) {  // wave-uniform: 128 tiles' words
+#pragma unroll
+                for (int q = 0; q < RW_REGS; ++q)
+                    wseg[(tiles_done - RW_REGS * TK5_WIN_TILES) * U + q * WAVE + lane] = grp[q];
+            }
+#endif
+            // TF 5 / 6: the entries staged before each window (lane w % 64 of
+            // wsr), so the staged top-k kernels take the windows independently
+            if constexpr (ORD)
+                if (tiles_done % TK5_WIN_TILES == 0) {  // wave-uniform
+                    const uint32_t wi = tiles_done / TK5_WIN_TILES;
+                    wsr = (uint32_t)lane == wi % WAVE ? os.seg_fill + os.wfill : wsr;
+                    if (wi % WAVE == WAVE - 1 && wi - (WAVE - 1) + lane < seg.nwin)
+                        seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + wi - (WAVE - 1) + lane] = wsr;
+                }
+        }
     }
-    if constexpr (TF >= 3)
-        if (pend_at != ~0ull) tflags[pend_at] = pend_word;
+    if constexpr (TF >= 3) {  // the last partial groups
+        const uint32_t g0 = tiles_done - tiles_done % (RW_REGS * TK5_WIN_TILES);  // first tile not stored
+#pragma unroll
+        for (int q = 0; q < RW_REGS; ++q) {
+            const uint32_t t0 = g0 + (uint32_t)q * TK5_WIN_TILES;
+            if (t0 < tiles_done && (uint32_t)lane < (tiles_done - t0 < TK5_WIN_TILES ? tiles_done - t0 : TK5_WIN_TILES) * U)
+                wseg[t0 * U + lane] = grp[q];
+        }
+        if constexpr (ORD) {
+            const uint32_t wl = tiles_done / TK5_WIN_TILES, w0 = wl - wl % WAVE;  // windows w0 .. wl not stored
+            if (wl % WAVE != WAVE - 1 && (uint32_t)lane <= wl % WAVE && w0 + lane < seg.nwin)
+                seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + w0 + lane] = wsr;
+        }
+    }
     // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;
     if (blockIdx.x == (uint32_t)(nfull % gridDim.x))

@@ -76,7 +76,8 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          uint32_t *__restrict__ tcnt,
                                                          const uint32_t *__restrict__ tflags, u64 head, u64 nfull,
-                                                         const SelState *__restrict__ st, u64 ncov) {
+                                                         const SelState *__restrict__ st, u64 ncov,
+                                                         RowWords rwl = RowWords{1, 0}) {
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
@@ -94,8 +95,8 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
         bool act = tl < ntiles;
         if (staged_ok && tl < ncov) act = false;  // counted by k_tk5_count
         if (act && meta_ok && tl < ncov) {
-            const uint32_t w0 = tflags[row_word(tl, 0)], w1 = tflags[row_word(tl, 1)], w2 = tflags[row_word(tl, 2)],
-                           w3 = tflags[row_word(tl, 3)];
+            const uint32_t w0 = tflags[rw_index(rwl, tl, 0)], w1 = tflags[rw_index(rwl, tl, 1)],
+                           w2 = tflags[rw_index(rwl, tl, 2)], w3 = tflags[rw_index(rwl, tl, 3)];
             if (((w0 | w1 | w2 | w3) & TK_RECOUNT) == 0u) {
                 tcnt[tl] += w0 + w1 + w2 + w3;  // k_topk_cands ran first: add to the candidates' share
                 act = false;
@@ -425,11 +426,12 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const Tk5Part P = tk5_part(nfull, G);
     const int32_t *sv = segv + (P.b * (TK_BLOCK / WAVE) + w) * seg_cap;
+    const uint32_t *ws = tflags + TF_W0 + (P.b * (TK_BLOCK / WAVE) + w) * rw_seg_words(nfull, G);  // this wave's row words
     for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
         const u64 j = win * WAVE + lane;
         const bool valid = j < P.m;
         const u64 r = (P.b + (j / MAIN_UNROLL) * P.G) * MAIN_UNROLL + j % MAIN_UNROLL;
-        const uint32_t c = valid ? tflags[row_word(r, (uint32_t)w)] : 0u;
+        const uint32_t c = valid ? ws[j] : 0u;
         const uint32_t start = tk5_wstart(wstart, nwin, P.b, w, win) + wave_incl_scan32(c) - c;
         uint32_t nb = 0, ne = 0;
         tk5_entries(sv + start, nullptr, c, [&](int32_t x, uint8_t) {
@@ -463,13 +465,13 @@ struct Tk5Rec {                  // one lane's row records of a window
     u64 off, b0, b1;             // toff[r], bbase[2 blk], bbase[2 blk + 1]
     uint4 wc;                    // the row's four wave-row words
 };
-__device__ __forceinline__ Tk5Rec tk5_rec(const uint32_t *__restrict__ tflags, const uint32_t *__restrict__ wcnt,
+__device__ __forceinline__ Tk5Rec tk5_rec(const uint32_t *__restrict__ ws, const uint32_t *__restrict__ wcnt,
                                           const uint32_t *__restrict__ tcnt, const u64 *__restrict__ toff,
-                                          const u64 *__restrict__ bbase, u64 r, bool valid, int w) {
+                                          const u64 *__restrict__ bbase, u64 r, u64 j, bool valid) {
     Tk5Rec x{0u, 0u, 0ull, 0ull, 0ull, make_uint4(0u, 0u, 0u, 0u)};
     if (valid) {
         const u64 blk = r / TK_TILES_PER_BLOCK;
-        x.c = tflags[row_word(r, (uint32_t)w)];
+        x.c = ws[j];
         x.tc = tcnt[r];
         x.off = toff[r];
         x.b0 = bbase[2 * blk];
@@ -506,13 +508,15 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
         return ((u64)(uint32_t)__shfl((int)(uint32_t)(x >> 32), l, WAVE) << 32) |
                (uint32_t)__shfl((int)(uint32_t)x, l, WAVE);
     };
-    Tk5Rec nx = tk5_rec(tflags, wcnt, tcnt, toff, bbase, row_of(P.w_lo * WAVE + lane), P.w_lo * WAVE + lane < m, w);
+    const uint32_t *ws = tflags + TF_W0 + (b * (TK_BLOCK / WAVE) + w) * rw_seg_words(nfull, G);  // this wave's row words
+    Tk5Rec nx = tk5_rec(ws, wcnt, tcnt, toff, bbase, row_of(P.w_lo * WAVE + lane), P.w_lo * WAVE + lane,
+                        P.w_lo * WAVE + lane < m);
     for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
         const u64 j0 = win * WAVE, j = j0 + lane;
         const bool valid = j < m;
         const u64 r = row_of(j);
         const Tk5Rec cur = nx;
-        if (win + 1 < P.w_hi) nx = tk5_rec(tflags, wcnt, tcnt, toff, bbase, row_of(j + WAVE), j + WAVE < m, w);
+        if (win + 1 < P.w_hi) nx = tk5_rec(ws, wcnt, tcnt, toff, bbase, row_of(j + WAVE), j + WAVE, j + WAVE < m);
         const uint32_t c = cur.c;
         const uint32_t start = tk5_wstart(wstart, nwin, b, w, win) + wave_incl_scan32(c) - c;
         // this row's bases, and this wave-row's (after the earlier quarters' counts)
