@@ -22,6 +22,8 @@
 
 namespace kth {
 
+#define KTH_STR2(x) #x
+#define KTH_STR(x) KTH_STR2(x)
 constexpr int BLK = 256;
 #ifndef KTH_MAIN_UNROLL
 #define KTH_MAIN_UNROLL 8
@@ -876,17 +878,24 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     // early finishers' bandwidth goes to the rest.  DESIGN.md.)
     auto load_tile = [&](uint4 (&x)[U], u64 t) {
         const uint4 *src = v + t * tile + threadIdx.x;
-        // Two loads, wait for the first, then the other U-2: the compiler's
-        // own order for k_main<0>.  Sending all U first (a sched_barrier after
-        // the loads, and the top-k variants' own schedule) made the pass slower:
-        // k_main<0> 640 -> 685 us, k_main<5> ~750 vs 640 at 2^30.
-        x[0] = load_nt(src);
-        x[1] = load_nt(src + BLK);
-#ifndef KTH_MAIN_NOWAIT1
-        if constexpr (TF != 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        // One load, wait for it, then the other U-1, in every variant.  Measured
+        // at 2^30 (k_main<0>, A/B in one process): the compiler's own order --
+        // two loads, wait for the first, then six -- 0.637 ms; one first
+        // 0.633 ms (select 1540 -> 1551 Gkeys/s); two then both 0.643; three
+        // or four then one 0.640-0.641; all eight first (a sched_barrier) 0.685;
+        // the next tile's first 1 / 2 / 4 loads issued before this tile is used
+        // 0.703 / 0.695 / 0.689.  The top-k variants' own schedule sent all
+        // eight first: k_main<5> ~750 us.  Fewer requests in flight per wave
+        // at a tile's start stream faster here, not more.
+#ifndef KTH_MAIN_FIRST  // design exploration: loads before the wait, and the wait's vmcnt
+#define KTH_MAIN_FIRST 1
+#define KTH_MAIN_WAITN 0
 #endif
 #pragma unroll
-        for (int u = 2; u < U; ++u) x[u] = load_nt(src + u * BLK);
+        for (int u = 0; u < KTH_MAIN_FIRST; ++u) x[u] = load_nt(src + u * BLK);
+        asm volatile("s_waitcnt vmcnt(" KTH_STR(KTH_MAIN_WAITN) ")" ::: "memory");
+#pragma unroll
+        for (int u = KTH_MAIN_FIRST; u < U; ++u) x[u] = load_nt(src + u * BLK);
     };
     // (Issuing the first tile's loads before the advance made the pass slower,
     // 656 vs 642 us: the advance's histogram loads then wait behind them.)
