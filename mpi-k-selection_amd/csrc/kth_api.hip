@@ -62,7 +62,7 @@ constexpr u64 FIN_SPARSE_PER_WG = (u64)kth::DENSE_BLK * kth::FIN_UNROLL * 4;  //
 constexpr double HEAD_SLACK = 1.5;  // k_head early window (EarlyWindow); KTH_HEAD_SLACK overrides, 0 = off
 static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
-constexpr u64 TK_STAGE_MAX_FRAC = 32;  // staged top-k (k_main<5/6>) for k <= n / 32
+constexpr u64 TK_STAGE_MAX_FRAC = 16;  // staged top-k (k_main<5/6>) for k <= n / 16
 constexpr int TK5_SPLIT = 4;            // workgroups per k_main workgroup in k_tk5_count / k_tk5_write (window-parallel)
 
 #define HIP_TRY(x)                                                                                    \
@@ -970,7 +970,7 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     //   small that the rows holding output are a few per cent (k * 64 Ki <=
     //   n: one flag bit per row, the count pass loads only flagged tiles,
     //   tf 1 / 2; measured ~equal there, and it needs no alignment)
-    //   and for n / 64 Ki < k <= n / 32 (16-byte aligned), every key on the
+    //   and for n / 64 Ki < k <= n / 16 (16-byte aligned), every key on the
     //   kept side of the window's far edge staged in index order (tf 5 / 6):
     //   neither the count nor the write pass reads the input (KTH_TOPK_STAGE=0: tf 3 / 4)
     const bool aligned = (reinterpret_cast<uintptr_t>(d_keys) & 15u) == 0;
@@ -1001,7 +1001,11 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     uint32_t nwin = 0;
     if (tf >= 5) {  // the staging segments: one per k_main wave, n / 16 entries in all
         const u64 nwaves = (u64)c->main_grid[tf] * (kth::BLK / kth::WAVE);
-        seg_cap = c->topk_seg_cap ? c->topk_seg_cap : (std::max<u64>(1ull << 20, (u64)n / 16) + nwaves - 1) / nwaves;
+        // entries: the k kept keys, the candidates (~0.6 % of n at 2^30) and the
+        // waves' imbalance; a segment that overflows sends the top-k to the
+        // input-reading path (exact)
+        const u64 seg_total = std::max<u64>({1ull << 20, (u64)n / 16, (u64)k + (u64)k / 8 + (u64)n / 64});
+        seg_cap = c->topk_seg_cap ? c->topk_seg_cap : (seg_total + nwaves - 1) / nwaves;
         KTH_TRY(reserve_cand(c, n));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segv), &c->tk_segv_cap, seg_cap * nwaves * 4));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segp), &c->tk_segp_cap, seg_cap * nwaves));
@@ -1078,7 +1082,8 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
                                                               c->st + c->last_state);
     kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
     if (tf >= 5) {
-        kth::k_tk5_write<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
+        auto tk5w = (u64)k * 32 <= (u64)n ? kth::k_tk5_write<kth::TK5_STAGE_SMALL> : kth::k_tk5_write<kth::TK5_STAGE_LARGE>;
+        tk5w<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
             c->tk_segv, c->tk_segp, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status,
             flip, c->tk_wcnt, tcnt, toff, bbase, meta, d_vals, d_idx);
         kth::k_topk_write<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,

@@ -641,7 +641,7 @@ struct Stager {
     }
 };
 
-// TF 5 / 6 (top-k, k smallest / largest, n/65536 < k <= n/32): every key on
+// TF 5 / 6 (top-k, k smallest / largest, n/65536 < k <= n/16): every key on
 // the kept side of the window's far edge (x <= hi / x >= lo: the keys certainly
 // in the output, the candidates and both edges) is staged IN INDEX ORDER with
 // its position in its wave-row (one byte) into the wave's own segment of the

@@ -459,7 +459,9 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
 // 300 us at k = 2^24).  A window whose output exceeds the stage is written
 // directly.  The next window's row records are loaded while this one is
 // placed and copied (the loop is a chain of dependent loads and barriers).
-constexpr int TK5_STAGE = 4096;  // output entries a workgroup stages (24 KiB of LDS: k_main's grid stays resident)
+// output entries a workgroup stages: 4096 (24 KiB of LDS) for k <= n / 32,
+// 8192 (48 KiB) above (a window of 64 Ki keys then holds ~k / n * 64 Ki outputs)
+constexpr int TK5_STAGE_SMALL = 4096, TK5_STAGE_LARGE = 8192;
 struct Tk5Rec {                  // one lane's row records of a window
     uint32_t c, tc;              // the wave-row's entries; the row's count word
     u64 off, b0, b1;             // toff[r], bbase[2 blk], bbase[2 blk + 1]
@@ -480,6 +482,7 @@ __device__ __forceinline__ Tk5Rec tk5_rec(const uint32_t *__restrict__ ws, const
     }
     return x;
 }
+template <int TK5_STAGE>
 __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restrict__ segv,
                                                         const uint8_t *__restrict__ segp, u64 seg_cap,
                                                         const uint32_t *__restrict__ wstart, uint32_t nwin, u64 G,

@@ -223,18 +223,20 @@ def _staged_cases(n, rng):
 
 @pytest.mark.parametrize("largest", [False, True])
 def test_topk_staged_index_order(gpu, largest):
-    """n / 65536 < k <= n / 32 on the window path, 16-byte aligned keys: the
+    """n / 65536 < k <= n / 16 on the window path, 16-byte aligned keys: the
     streaming pass stages every key on the kept side of the window's far edge in
     index order per wave-row, with its position, in per-wave segments
     (k_main<5/6>), and the count and write passes read those entries, not the
     input (k_tk5_count, k_tk5_write); the ragged tail past the full tiles is
-    counted and written from the input.  Against a stable argsort."""
+    counted and written from the input.  k > n / 32 takes the larger LDS stage
+    of k_tk5_write; windows whose output exceeds the stage (sorted inputs: every
+    key of a window kept) are written directly.  Against a stable argsort."""
     import torch
     n = (1 << 23) + 4099
     rng = np.random.default_rng(41 + largest)
     for name, a in _staged_cases(n, rng):
         d = torch.from_numpy(a).cuda()
-        for k in (n // 65536 + 1, n // 1024, n // 256, n // 64, n // 32):
+        for k in (n // 65536 + 1, n // 1024, n // 256, n // 64, n // 32, n // 24, n // 16):
             vals, idx = _run(gpu, d, n, k, largest)
             want = _ref_idx(a, k, largest)
             np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"{name} k={k}")

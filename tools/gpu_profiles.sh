@@ -1,4 +1,4 @@
-# The round's committed evidence: bench line (+ CPU baselines), rocprof kernel
+# The round's committed evidence: the default bench line (+ CPU baselines), rocprof kernel
 # stats, PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes) for the
 # select path, and the same for the batched-rows path (int32 and f32).
 set -o pipefail
@@ -16,7 +16,7 @@ echo "== select: PMC"
 pmc select k_main 30 uniform_half -- --steps 3 --warmup 1 --no-cpu-baseline
 cp $O/pmc_traffic_select.json profiles/pmc_traffic.json
 echo "== select: bench"
-timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 > $O/bench.log 2>&1 || { echo bench rc=$?; tail -20 $O/bench.log; exit 1; }
+timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1 || { echo bench rc=$?; tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
 echo "== select: rocprof"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_select -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_select.log 2>&1 || { echo prof rc=$?; tail -20 $O/prof_select.log; exit 1; }
