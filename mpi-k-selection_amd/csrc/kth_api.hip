@@ -985,8 +985,10 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     // tflags: the header and TF 1 / 2's flag bytes after 4 words, TF >= 3's
     // row words after TF_W0 in per-wave segments (kth::rw_index); 256-byte
     // aligned, so that a wave's group of 64 words fills one line
-    const kth::RowWords rwl{(u64)c->main_grid[tf], kth::rw_seg_words(nfull, (u64)c->main_grid[tf])};
-    const u64 fwords = tf >= 3 ? kth::TF_W0 + rwl.G * (kth::BLK / kth::WAVE) * rwl.seg : 4 + nfull;
+    const u64 Gm = (u64)c->main_grid[tf];
+    const kth::RowWords rwl{Gm, tf >= 3 ? kth::rw_seg_words(nfull, Gm) : kth::fl_seg_bytes(nfull, Gm)};
+    const u64 fwords = tf >= 3 ? kth::TF_W0 + rwl.G * (kth::BLK / kth::WAVE) * rwl.seg
+                               : 4 + rwl.G * (kth::BLK / kth::WAVE) * rwl.seg / 4;
     const u64 fw64 = (fwords + 1) / 2, before = (ntiles + 1) / 2 + ntiles + 4 * nblk + 2;
     const u64 words = before + fw64 + 32;
     KTH_TRY(grow(reinterpret_cast<void **>(&c->topk), &c->topk_cap, words * sizeof(u64)));
@@ -1042,10 +1044,10 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
                                                                           tcnt, tflags, head, nfull, sel_st, ncov, rwl);
     } else if (aligned) {
         kth::k_topk_count<true, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
-                                                                           tcnt, tflags, head, nfull, sel_st, 0);
+                                                                           tcnt, tflags, head, nfull, sel_st, 0, rwl);
     } else {
         kth::k_topk_count<false, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
-                                                                            tcnt, tflags, head, nfull, sel_st, 0);
+                                                                            tcnt, tflags, head, nfull, sel_st, 0, rwl);
     }
     if (getenv("KTH_TOPK_DEBUG")) {  // diagnostic: tile counts against a host recount
         (void)hipStreamSynchronize(c->stream);

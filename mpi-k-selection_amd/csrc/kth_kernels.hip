@@ -810,7 +810,7 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
 // TF (top-k variant, kth_topk.hpp): 0 = plain select; 1 / 2 = also record, per
 // full tile, wave and row (the tile's u-th run of 4 * BLK keys), one bit "some
 // key <= hi" (1, k smallest) or "some key >= lo" (2, k largest): bit u of
-// ((uint8_t *)(tflags + 4))[4 * tile + wave]; and the window as tflags[0..2] =
+// ((uint8_t *)(tflags + 4))[fl_index(tile, wave)]; and the window as tflags[0..2] =
 // {lo, hi, 1} (signed).  A row with no bit set in any wave holds no output key
 // of the top-k when its k-th lies inside the window.
 // 3 / 4 (k smallest / largest, k > n / 1024): per full tile, row u and wave,
@@ -840,6 +840,14 @@ struct RowWords {
 };
 __host__ __device__ __forceinline__ u64 rw_seg_words(u64 nfull, u64 G) {
     return ((nfull + G - 1) / G * MAIN_UNROLL + 63) / 64 * 64;
+}
+// k_main<1/2>'s flag bytes (one per wave and tile, bit u = row u), the same
+// way: wave-major segments of `seg` bytes (tiles per workgroup, rounded up to
+// 256), byte i = the workgroup's tile i, after tflags' 16-byte header; a wave
+// collects 256 tiles' bytes in one register of its 64 lanes.
+__host__ __device__ __forceinline__ u64 fl_seg_bytes(u64 nfull, u64 G) { return ((nfull + G - 1) / G + 255) / 256 * 256; }
+__host__ __device__ __forceinline__ u64 fl_index(const RowWords &L, u64 t, uint32_t w) {
+    return ((t % L.G) * (BLK / WAVE) + w) * L.seg + t / L.G;
 }
 __host__ __device__ __forceinline__ u64 rw_index(const RowWords &L, u64 r, uint32_t w) {
     const u64 t = r / MAIN_UNROLL;
@@ -956,7 +964,11 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     // TF >= 3: lanes 0..U-1 leave the tile's row words in tile_word; lane
     // 8 (i % 8) + u of grp collects row u of the workgroup's tile i, and the
     // 64 lanes store every 8th tile (rw_index)
-    uint32_t tile_word = 0, grp[RW_REGS], wsr = 0;
+    uint32_t tiles_done = 0;  // TF >= 1: this workgroup's tiles so far
+    uint32_t tile_word = 0, grp[RW_REGS], wsr = 0, facc = 0;
+    uint32_t *const fseg = TF == 1 || TF == 2
+                               ? tflags + 4 + ((u64)blockIdx.x * (BLK / WAVE) + wid) * (fl_seg_bytes(nfull, gridDim.x) / 4)
+                               : nullptr;
 #pragma unroll
     for (int q = 0; q < RW_REGS; ++q) grp[q] = 0u;
     const u64 seg_words = rw_seg_words(nfull, gridDim.x);
@@ -972,7 +984,8 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 const bool nr = TF == 1 ? min(min(a0, a1), min(a2, a3)) <= shi : max(max(a0, a1), max(a2, a3)) >= slo;
                 rows |= (__builtin_amdgcn_ballot_w64(nr) != 0 ? 1u : 0u) << u;
             }
-            if (lane == 0) reinterpret_cast<uint8_t *>(tflags + 4)[4 * t + wid] = (uint8_t)rows;
+            // byte tiles_done % 4 of lane (tiles_done / 4) % 64 (stored every 256 tiles)
+            facc = (uint32_t)lane == (tiles_done / 4) % WAVE ? facc | rows << (8 * (tiles_done % 4)) : facc;
         }
 #ifdef KTH_DIAG_NOROWW  // diagnostic builds only (wrong top-k results): cost of the row words
         if constexpr (TF >= 5) {
@@ -1023,7 +1036,6 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         }
     };
     static_assert(TK5_WIN_TILES * U == WAVE, "a group of row words is one window of the staged kernels");
-    uint32_t tiles_done = 0;  // TF >= 3: this workgroup's tiles so far
     for (u64 t = blockIdx.x; t < nfull; t += gridDim.x) {
         uint4 x[U];
         RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
@@ -1042,6 +1054,13 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         } else {
             scan_tile(x, t, ra);
             flag_tile(x, t, ra, e0, c0);
+        }
+        if constexpr (TF == 1 || TF == 2) {
+            ++tiles_done;
+            if (tiles_done % (4 * WAVE) == 0) {  // wave-uniform: 256 tiles' bytes
+                fseg[(tiles_done - 4 * WAVE) / 4 + lane] = facc;
+                facc = 0;
+            }
         }
         if constexpr (TF >= 3) {
             // lane 8 (i % 8) + u of grp[(i / 8) % RW_REGS] <- row u of tile i
@@ -1068,6 +1087,10 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                         seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + wi - (WAVE - 1) + lane] = wsr;
                 }
         }
+    }
+    if constexpr (TF == 1 || TF == 2) {  // the last partial word group
+        const uint32_t left = tiles_done % (4 * WAVE);
+        if (left != 0 && (uint32_t)lane < (left + 3) / 4) fseg[(tiles_done - left) / 4 + lane] = facc;
     }
     if constexpr (TF >= 3) {  // the last partial groups
         const uint32_t g0 = tiles_done - tiles_done % (RW_REGS * TK5_WIN_TILES);  // first tile not stored

@@ -43,8 +43,10 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
 // `head` unaligned keys; MAIN_UNROLL rows per tile, nfull tiles) whose rows
 // carry no flag bit has no key <= v (>= v for largest): count 0, no loads.
 constexpr u64 TK_MAIN_ROW = (u64)BLK * 4;  // keys per k_main row (one 16-B load per thread)
-__device__ __forceinline__ bool tk_row_flagged(const uint32_t *fw, u64 r) {
-    return (fw[r / MAIN_UNROLL] & (0x01010101u << (r % MAIN_UNROLL))) != 0u;
+__device__ __forceinline__ bool tk_row_flagged(const uint8_t *fb, const RowWords &fl, u64 r) {
+    const u64 t = r / MAIN_UNROLL;
+    const uint32_t bit = 1u << (r % MAIN_UNROLL);
+    return ((fb[fl_index(fl, t, 0)] | fb[fl_index(fl, t, 1)] | fb[fl_index(fl, t, 2)] | fb[fl_index(fl, t, 3)]) & bit) != 0u;
 }
 
 // META (after k_main<3/4>, 16-byte aligned keys): the first ncov tiles are
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
     const bool meta_ok = META && tk_meta_ok(tflags, d_v, st);
     const bool staged_ok = MODE == 2 && tk5_ok(tflags, d_v);
     const uint32_t mark = meta_ok ? TK_RECOUNT : 0u;
-    const uint32_t *fw = tflags + 4;
+    const uint8_t *fb = reinterpret_cast<const uint8_t *>(tflags + 4);  // MODE 0: k_main<1/2>'s flag bytes (rwl: fl_index)
     // each wave takes 64 tiles at a time: lane l tests tile tg + l's flags, the
     // wave then streams only the tiles that may hold output
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE) * WAVE; tg < ntiles; tg += nw * WAVE) {
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
         if (act && skip_ok && tl * TK_TILE >= head) {
             const u64 b0 = tl * TK_TILE, last = (b0 + TK_TILE < n ? b0 + TK_TILE : n) - 1;
             const u64 ra = (b0 - head) / TK_MAIN_ROW, rb = (last - head) / TK_MAIN_ROW;
-            if (rb / MAIN_UNROLL < nfull && !tk_row_flagged(fw, ra) && !tk_row_flagged(fw, rb)) {
+            if (rb / MAIN_UNROLL < nfull && !tk_row_flagged(fb, rwl, ra) && !tk_row_flagged(fb, rwl, rb)) {
                 act = false;
                 tcnt[tl] = 0u;
             }
