@@ -590,7 +590,15 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     }
     const uint32_t my = (uint32_t)lane < L ? hist[lane] : 0u;
     uint32_t lt = 0, le = 0;
-    for (uint32_t i = 0; i < L; ++i) {  // wave-uniform trip count, broadcast reads
+    // wave-uniform trip counts, broadcast reads: four list keys a 16-byte read
+    // (one read and no loop bookkeeping per key), then the last L % 4
+    uint32_t i = 0;
+    for (; i + 4 <= L; i += 4) {
+        const uint4 y = *reinterpret_cast<const uint4 *>(hist + i);
+        lt += (y.x < my ? 1u : 0u) + (y.y < my ? 1u : 0u) + (y.z < my ? 1u : 0u) + (y.w < my ? 1u : 0u);
+        le += (y.x <= my ? 1u : 0u) + (y.y <= my ? 1u : 0u) + (y.z <= my ? 1u : 0u) + (y.w <= my ? 1u : 0u);
+    }
+    for (; i < L; ++i) {
         const uint32_t y = hist[i];
         lt += y < my ? 1u : 0u;
         le += y <= my ? 1u : 0u;
