@@ -42,6 +42,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def emit(obj):
+    """One JSON result line in ONE write(2): rank processes share the parent's
+    stdout, and print() writes the text and the newline separately, so two
+    ranks' lines could interleave."""
+    sys.stdout.flush()
+    data = (json.dumps(obj) + "\n").encode()
+    while data:
+        data = data[os.write(1, data):]
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -341,7 +351,7 @@ def rows_main(args):
         "verified": verified,
     }
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.destroy_process_group()
     return 0 if verified else 1
@@ -431,7 +441,7 @@ def topk_main(args):
         "verified": verified,
     }
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.destroy_process_group()
     return 0 if verified else 1
@@ -448,6 +458,8 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="global 1-based rank (default n_total/2)")
     ap.add_argument("--cpu-log2n", type=int, default=20, help="CPU baseline size (BASELINE config 1: 2^20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--local-shards", type=int, default=1,
+                    help="P > 1: P shards of 2^log2n keys on this one GPU through kth_sharded_* (config 3 on one GPU)")
     ap.add_argument("--dist", action="store_true",
                     help="run the sharded (kth_dist_* + RCCL) protocol even on one GPU")
     ap.add_argument("--workload", choices=["select", "rows", "topk"], default="select",
@@ -470,8 +482,7 @@ def main():
         log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run as {args.gpus}")
         return 2
     if args.probe_launch:
-        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
-                                                          "MASTER_PORT")}), flush=True)
+        emit({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")})
         return 0
     if args.workload == "rows":
         return rows_main(args)
@@ -503,16 +514,32 @@ def main():
 
     sel = kselect.Selector(local_rank)
     sel.set_stream(torch.cuda.current_stream(dev))
+    P = args.local_shards
+    if P > 1 and sharded:
+        raise SystemExit("bench: --local-shards runs on one GPU without --dist / WORLD_SIZE > 1")
     n_local = 1 << args.log2n
-    n_total = n_local * world
+    n_total = n_local * world * P
     k = args.k or n_total // 2
     family = kselect.FAMILIES[args.family]
-    keys = torch.empty(n_local, dtype=torch.int32, device=dev)
-    sel.fill(keys, n_local, family, args.seed, offset=rank * n_local, n_total=n_total)
+    keys = torch.empty(n_local * P, dtype=torch.int32, device=dev)
+    sel.fill(keys, n_local * P, family, args.seed, offset=rank * n_local, n_total=n_total)
     out = torch.zeros(args.warmup + args.steps, dtype=torch.int32, device=dev)
     comm_world = None
+    local_answers = [0] * (args.warmup + args.steps)
 
-    if not sharded:
+    if P > 1:
+        # BASELINE config 3's shards on ONE GPU: P shards of 2^log2n keys
+        # through kth_sharded_* with the device repeated (the local
+        # transport: the same per-shard steps, the all-reduces a device-side
+        # slot sum).  kth_sharded_select_i32 is synchronous: each step ends
+        # with the answer on the host.
+        views = [keys[i * n_local:(i + 1) * n_local] for i in range(P)]
+        sh = kselect.ShardedSelector([local_rank] * P)
+        sizes = [n_local] * P
+
+        def step(i):
+            local_answers[i] = sh.select(views, k, sizes)
+    elif not sharded:
         sel.reserve(n_local)
 
         def step(i):
@@ -530,51 +557,56 @@ def main():
         step(i)
     torch.cuda.synchronize()
     barrier()
-    sel.enable_timing(True)
-    torch.cuda.synchronize()
-    barrier()
+    # the timed region: exactly K steps, no HIP timing events on the stream
+    # (events switch the queue to timestamped dispatches, ~10 us a select)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
     barrier()
-    n_sel, main_ms, total_ms = sel.take_timing()
-    elapsed = t1 - t0
-    # the same steps once more with no HIP events on the stream (diagnostic:
-    # timing events switch the queue to timestamped dispatches, ~10 us a select)
-    sel.enable_timing(False)
+    # then the same K steps once more with events around the streaming pass
+    # and each whole select: roofline.avg_launch_ms (not the value)
+    sel.enable_timing(True)
     torch.cuda.synchronize()
     barrier()
     t2 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     torch.cuda.synchronize()
-    elapsed_ne = time.perf_counter() - t2
+    elapsed_ev = time.perf_counter() - t2
+    barrier()
+    n_sel, main_ms, total_ms = sel.take_timing()
+    sel.enable_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed_ne], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed_ne = float(t.item())
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, elapsed_ev = (float(x) for x in t.tolist())
 
     # exact rank certificate of every answer (device-side integer counts)
-    answers = out.cpu().tolist()
+    answers = local_answers if P > 1 else out.cpu().tolist()
     v = answers[args.warmup]
-    cnt = torch.stack([(keys < v).sum(), (keys <= v).sum()]).to(torch.int64)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    for c in torch.split(keys, 1 << 30):  # (bounded temporaries at 2^33)
+        cnt += torch.stack([(c < v).sum(), (c <= v).sum()]).to(torch.int64)
     if world > 1:
         dist.all_reduce(cnt)
     lt, le = (int(x) for x in cnt.tolist())
     verified = (lt < k <= le) and all(a == v for a in answers)
-    stats = sel.stats() if not sharded else None
+    stats = sel.stats() if not sharded and P == 1 else None
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = n_total / (elapsed / args.steps) / 1e9
     avg_main_ms = main_ms / max(1, n_sel)
     achieved = 4.0 * n_local / (avg_main_ms * 1e-3) / 1e9 if avg_main_ms > 0 else None
+    kernel = "kth::k_main (streaming pass)"
+    if P > 1:  # the shards' ctxs are internal to the handle: the whole select, host-timed
+        avg_main_ms = ms_per_step
+        achieved = 4.0 * n_local * P / (ms_per_step * 1e-3) / 1e9
+        kernel = f"whole sharded select ({P} shards on one GPU, host-timed, synchronous)"
     traffic, traffic_note = pmc_traffic("pmc_traffic.json", args.log2n, args.family)
+    if P > 1:
+        traffic, traffic_note = None, "PMC traffic is measured per k_main launch (one shard), not per sharded select"
 
     res = {
         "metric": "Gkeys/s exact k-th select, 2^30 int32 (1 GPU) / 2^33 (8 GPU); % HBM roofline",
@@ -590,30 +622,32 @@ def main():
         "dtype": "int32",
         "data": "synthetic (device counter-based generator, splitmix64)",
         "config": {
-            "workload": f"exact k-th select (median) of 2^{args.log2n} int32 keys per GPU, {args.family}",
+            "workload": (f"exact k-th select (median) of 2^{args.log2n} int32 keys per GPU, {args.family}" if P == 1 else
+                         f"BASELINE config 3 on one GPU: exact k-th select (median) of {P} shards x 2^{args.log2n} "
+                         f"int32 keys (kth_sharded local transport), {args.family}"),
             "n_total": n_total,
             "k": k,
             "keys_per_gpu": n_local,
             "family": args.family,
-            "parallelism": f"shards{world}" if sharded else "single",
+            "parallelism": f"shards{world}" if sharded else (f"local_shards{P}" if P > 1 else "single"),
             "rccl_world": comm_world if sharded else None,
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "kth::k_main (streaming pass)",
+            "kernel": kernel,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
             "traffic_source": traffic_note,
-            "algorithmic_bytes_per_launch": 4 * n_local,
+            "algorithmic_bytes_per_launch": 4 * n_local * P,
             "avg_launch_ms": avg_main_ms,
         },
         "verified": bool(verified),
         "answer": v,
         "whole_select_ms_events": total_ms / max(1, n_sel) if not sharded else None,
-        "ms_per_step_no_events": elapsed_ne * 1e3 / args.steps,
+        "ms_per_step_events": elapsed_ev * 1e3 / args.steps,
     }
     if stats:
         res["path"] = {1: "lds", 2: "radix", 3: "window", 4: "window_fallback"}.get(stats["path"], "?")
@@ -632,7 +666,7 @@ def main():
         res["cpu_host"] = host
 
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if sharded:
         dist.destroy_process_group()
     return 0 if verified else 1

@@ -217,7 +217,12 @@ int kth_window_slack64(void);
  * with the collectives as grouped RCCL calls over communicators from
  * ncclCommInitAll (RCCL is dlopen'ed at first use: the librccl.so.1 already in
  * the process, else the system one; KTH_ECOMM if neither loads).
- *   kth_sharded_create      devices[0..ngpu) distinct; one ctx, stream and
+ * Local transport: ngpu > 1 copies of ONE device id (at most 64) put every
+ * shard on that device with no RCCL: the same per-shard steps on one shared
+ * stream, the samples gathered in place, each all-reduce a device-side sum of
+ * the shards' slots (P shards of a 2^33-key input on one GPU).
+ *   kth_sharded_create      devices[0..ngpu) distinct (RCCL), or all equal
+ *                           (local); one ctx per shard, one stream and
  *                           communicator per device
  *   kth_sharded_select_i32  shard i = shards[i][0..shard_n[i]) in device
  *                           devices[i]'s memory; k-th smallest (1-based) of the
@@ -237,6 +242,12 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
                            int32_t *out);
 int kth_select_i32_sharded(const int32_t *const *dev_shards, const int64_t *shard_n, int ngpu, int64_t k,
                            int32_t *out);
+/* Per-shard sample sizes of kth_sharded_select_i32: about
+ * kth_dist_sample_size(n_total) keys in all, split in proportion to the shard
+ * sizes, each a multiple of 64, at least 64 and at most the shard rounded down
+ * to 64.  Writes s_dev[0..P), returns their sum (KTH_EINVAL for bad input).
+ * Host-only arithmetic (no device needed). */
+int64_t kth_sharded_sample_split(const int64_t *shard_n, int P, int64_t *s_dev);
 /* Diagnostics: host microseconds the last kth_sharded_select_i32 on h spent
  * enqueueing device work and collectives for every device (from its entry to
  * the last kth_dist_result enqueue; the wait for the answer excluded); -1 for

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "kth.h"
+#include "kth_internal.h"
 #include "kth_kernels.hip"
 #include "kth_topk.hpp"
 
@@ -64,6 +65,7 @@ static_assert(KTH_STATS_WORDS == kth::STATS_WORDS, "include/kth.h slot size");
 constexpr int MAX_EVENTS = 4 * 2048;
 constexpr u64 TK_STAGE_MAX_FRAC = 16;  // staged top-k (k_main<5/6>) for k <= n / 16
 constexpr int TK5_SPLIT = 4;            // workgroups per k_main workgroup in k_tk5_count / k_tk5_write (window-parallel)
+constexpr int COOP_BACKOFF = 64;        // synchronous selects on the per-level path after a grid-barrier timeout
 
 #define HIP_TRY(x)                                                                                    \
     do {                                                                                              \
@@ -93,6 +95,8 @@ struct kth_ctx {
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
     bool coop = true;          // window / radix paths as k_head + k_main + k_finish (KTH_COOP=0: per-level launches)
+    bool coop_wanted = true;   // coop as configured (env, LDS, residency); coop may be off for a while after a timeout
+    int coop_backoff = 0;      // synchronous selects left on the per-level path after a grid-barrier timeout
     bool coop_resident = true; // the cooperative grids fit the device at once (occupancy check at ctx creation)
     int fin_grid = 256;        // k_finish workgroups (one per CU; KTH_FIN_GRID)
     uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
@@ -716,8 +720,12 @@ int kth_ctx_create(int device, kth_ctx **out) {
         // the cooperative path when the device cannot hold the grid (a plain
         // launch checks nothing).  Residency can still be taken away at run
         // time by other streams or processes: the spins are bounded, a timeout
-        // is reported (state error ERR_BARRIER, d_out untouched) and the
-        // synchronous entry points redo the select on the per-level path.
+        // is reported (state error ERR_BARRIER, d_out untouched) and
+        // kth_select_i32_ctx (hence kth_select_i32 and VecKthSelect) redoes the
+        // select on the per-level path and stays on it for the next
+        // COOP_BACKOFF synchronous selects.  The asynchronous entry points
+        // (kth_select_i32_async, kth_topk_i32, kth_dist_*) report the error in
+        // the state (kth_ctx_last_stats) and leave the retry to the caller.
         {
             int fin_per_cu = 0, head_per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&fin_per_cu, reinterpret_cast<const void *>(kth::k_finish),
@@ -733,6 +741,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             }
         }
     } while (0);
+    c->coop_wanted = c->coop;
     if (rc != KTH_OK) {
         kth_ctx_destroy(c);
         return rc;
@@ -808,6 +817,7 @@ int kth_select_i32_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k
 int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *out) {
     if (!c || !keys || !out || n < 1 || k < 1 || k > n) return KTH_EINVAL;
     KTH_TRY(set_device(c));
+    if (c->coop_backoff > 0 && --c->coop_backoff == 0) c->coop = c->coop_wanted;  // try the grid barriers again
     const int32_t *dk = keys;
     if (!is_device_ptr(keys)) {
         KTH_TRY(grow(reinterpret_cast<void **>(&c->staging), &c->staging_cap, (u64)n * 4));
@@ -821,11 +831,12 @@ int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, in
         // a cooperative grid was not co-resident (another stream or process
         // held CUs): redo the select on the per-level path, which needs no
         // residency; the slots are re-zeroed first (dirty)
+        // (sticky for COOP_BACKOFF synchronous selects: while the CUs stay
+        // contended, every cooperative launch would spin out its barriers)
         c->dirty = true;
         c->coop = false;
-        const int rc = select_async(c, dk, n, k, nullptr, c->d_status);
-        c->coop = true;
-        KTH_TRY(rc);
+        c->coop_backoff = COOP_BACKOFF;
+        KTH_TRY(select_async(c, dk, n, k, nullptr, c->d_status));
         HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
@@ -1248,6 +1259,19 @@ int kth_dist_level(kth_ctx *c, const int32_t *d_keys, int64_t n_local, int level
     KTH_TRY(launch_check());
     c->dist_level_next = level + 1;
     return acc;
+}
+
+int kth_internal_slots_sum(uint64_t *const *slots, int P, int slot, void *stream) {
+    static_assert(kth::SLOTS_SUM_MAX == KTH_LOCAL_MAX_SHARDS, "one limit");
+    if (!slots || P < 1 || P > KTH_LOCAL_MAX_SHARDS || slot < 0 || slot > 2) return KTH_EINVAL;
+    kth::SlotPtrs s{};
+    for (int i = 0; i < P; ++i) {
+        if (!slots[i]) return KTH_EINVAL;
+        s.p[i] = reinterpret_cast<u64 *>(slots[i]) + (size_t)slot * KTH_STATS_WORDS;
+    }
+    constexpr int g = (KTH_STATS_WORDS + kth::BLK - 1) / kth::BLK;
+    kth::k_slots_sum<<<g, kth::BLK, 0, reinterpret_cast<hipStream_t>(stream)>>>(s, P, (u64)KTH_STATS_WORDS);
+    return launch_check();
 }
 
 int kth_dist_result(kth_ctx *c, int32_t *d_out) {

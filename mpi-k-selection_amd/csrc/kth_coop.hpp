@@ -43,7 +43,7 @@ struct CoopArgs {
     u64 zero2_words;
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
     uint32_t sample_ready;  // k_head: the sample (order keys) is already in `sample` (sharded window)
-    uint32_t fault;    // test hook (KTH_FAULT_BARRIER): the first grid barrier reports a timeout
+    uint32_t fault;    // test hook (KTH_FAULT_BARRIER): the grid barriers report a timeout
 };
 
 // This wave's outstanding global accesses (atomics, write-through stores) are
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     bool ok = true;
     for (int L = 0;; ++L) {
         grid_sync(gb, s_base, ok);
+        if (x.fault) ok = false;  // test hook: as if this barrier had timed out
         if (L == 0) KTH_STAMP(a, 2);
         if (L == 1) KTH_STAMP(a, 5);
         pick_slot<DENSE_BLK>(ss, x.slots + (size_t)L * STATS_WORDS, share, scratch, &ew);

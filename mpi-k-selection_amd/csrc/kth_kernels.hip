@@ -1337,6 +1337,21 @@ __global__ __launch_bounds__(BLK) void k_fill(int32_t *__restrict__ out, u64 n, 
     }
 }
 
+// The local transport of a one-device sharded handle (kth_sharded.cpp): the
+// all-reduce of one stats slot across the shards' slot buffers -- each word
+// summed over the P shards and written back to every one of them.
+constexpr int SLOTS_SUM_MAX = 64;  // == KTH_LOCAL_MAX_SHARDS
+struct SlotPtrs {
+    u64 *p[SLOTS_SUM_MAX];
+};
+__global__ __launch_bounds__(BLK) void k_slots_sum(SlotPtrs s, int P, u64 words) {
+    for (u64 i = (u64)blockIdx.x * BLK + threadIdx.x; i < words; i += (u64)gridDim.x * BLK) {
+        u64 sum = 0;
+        for (int r = 0; r < P; ++r) sum += s.p[r][i];
+        for (int r = 0; r < P; ++r) s.p[r][i] = sum;
+    }
+}
+
 }  // namespace kth
 
 #include "kth_coop.hpp"

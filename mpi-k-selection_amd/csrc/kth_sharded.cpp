@@ -18,6 +18,15 @@
 // the end to read the answer.  RCCL is resolved at first use (dlopen of the
 // librccl.so.1 already in the process, e.g. torch's, or the system one), so
 // libkth.so itself does not depend on it.
+//
+// Local transport: a handle whose shards all live on ONE device (the same
+// device id repeated, e.g. 8 shards x 2^30 keys on one MI355X) runs the same
+// per-shard steps with no RCCL: every shard's ctx enqueues on one shared
+// stream (so each step sees the previous step of every shard complete), the
+// samples are written straight into one gathered buffer at their offsets (the
+// all-gather), and each all-reduce is one small kernel that sums the shards'
+// slot words and writes the sum back to every shard's slot
+// (kth_internal_slots_sum) -- the arithmetic RCCL's ncclSum performs.
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -29,6 +38,7 @@
 #include <vector>
 
 #include "kth.h"
+#include "kth_internal.h"
 
 namespace {
 
@@ -93,6 +103,7 @@ struct Dev {
     int device = 0;
     kth_ctx *ctx = nullptr;
     hipStream_t stream = nullptr;
+    bool own_stream = false;  // local transport: shard 0 owns the shared stream
     ncclComm_t comm = nullptr;
     uint64_t *slots = nullptr;  // 3 * KTH_STATS_WORDS
     uint32_t *sample = nullptr, *gathered = nullptr;
@@ -122,6 +133,9 @@ int grow(int device, void **p, int64_t *cap, int64_t bytes) {
 
 struct kth_sharded {
     std::vector<Dev> d;
+    bool local = false;           // every shard on one device: the local transport (no RCCL)
+    uint32_t *lgathered = nullptr;  // local transport: the gathered sample (every shard's at its offset)
+    int64_t lgathered_cap = 0;
     double enqueue_us = 0;  // host time of the last select up to its last enqueue (kth_sharded_enqueue_us)
 };
 
@@ -134,10 +148,13 @@ int select_gathered(kth_sharded *h, const int32_t *const *shards, const int64_t 
     Dev &d0 = h->d[0];
     TRY(grow(d0.device, reinterpret_cast<void **>(&d0.staging), &d0.staging_cap, std::max<int64_t>(n_total, 1) * 4));
     HIPT(hipSetDevice(d0.device));
-    for (Dev &x : h->d) HIPT(hipStreamSynchronize(x.stream));  // callers' earlier work on the shards
+    for (Dev &x : h->d) HIPT(hipStreamSynchronize(x.stream));  // the handle's earlier work on the shards
     int64_t off = 0;
     for (size_t i = 0; i < h->d.size(); ++i) {
-        if (shard_n[i] > 0)
+        if (shard_n[i] > 0 && h->d[i].device == d0.device)
+            HIPT(hipMemcpyAsync(d0.staging + off, shards[i], (size_t)shard_n[i] * 4, hipMemcpyDeviceToDevice,
+                                d0.stream));
+        else if (shard_n[i] > 0)
             HIPT(hipMemcpyPeerAsync(d0.staging + off, d0.device, shards[i], h->d[i].device, (size_t)shard_n[i] * 4,
                                     d0.stream));
         off += shard_n[i];
@@ -161,7 +178,15 @@ int kth_sharded_destroy(kth_sharded *h) {
         if (x.out) (void)hipFree(x.out);
         if (x.staging) (void)hipFree(x.staging);
         if (x.ctx) (void)kth_ctx_destroy(x.ctx);  // before its stream: it synchronises on it
-        if (x.stream) (void)hipStreamDestroy(x.stream);
+    }
+    for (Dev &x : h->d)  // (local transport: one stream, owned by shard 0)
+        if (x.stream && x.own_stream) {
+            (void)hipSetDevice(x.device);
+            (void)hipStreamDestroy(x.stream);
+        }
+    if (h->lgathered) {
+        (void)hipSetDevice(h->d[0].device);
+        (void)hipFree(h->lgathered);
     }
     delete h;
     return KTH_OK;
@@ -173,13 +198,20 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
     if (!devices || ngpu < 1) return KTH_EINVAL;
     const int ndev = kth_device_count();
     if (ndev <= 0) return KTH_ENODEV;
+    // distinct devices: RCCL, one rank per device; the same device repeated:
+    // the local transport (any other repetition is refused)
+    bool all_same = true, distinct = true;
     for (int i = 0; i < ngpu; ++i) {
         if (devices[i] < 0 || devices[i] >= ndev) return KTH_EINVAL;
-        for (int j = 0; j < i; ++j)
-            if (devices[j] == devices[i]) return KTH_EINVAL;  // RCCL needs one rank per device
+        all_same = all_same && devices[i] == devices[0];
+        for (int j = 0; j < i; ++j) distinct = distinct && devices[j] != devices[i];
     }
-    if (!rccl().ok) return KTH_ECOMM;
+    const bool local = ngpu > 1 && all_same;
+    if (!local && !distinct) return KTH_EINVAL;
+    if (local && ngpu > KTH_LOCAL_MAX_SHARDS) return KTH_EINVAL;
+    if (!local && !rccl().ok) return KTH_ECOMM;
     kth_sharded *h = new kth_sharded();
+    h->local = local;
     h->d.resize((size_t)ngpu);
     int rc = KTH_OK;
     std::vector<ncclComm_t> comms((size_t)ngpu, nullptr);
@@ -187,10 +219,17 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
         Dev &x = h->d[(size_t)i];
         x.device = devices[i];
         if ((rc = kth_ctx_create(x.device, &x.ctx)) != KTH_OK) break;
-        if (hipSetDevice(x.device) != hipSuccess ||
-            hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipSetDevice(x.device) != hipSuccess) {
             rc = KTH_EHIP;
             break;
+        }
+        if (local && i > 0) {
+            x.stream = h->d[0].stream;  // one stream for every shard of the device
+        } else if (hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking) != hipSuccess) {
+            rc = KTH_EHIP;
+            break;
+        } else {
+            x.own_stream = true;
         }
         if ((rc = kth_ctx_set_stream(x.ctx, x.stream)) != KTH_OK) break;
         if (hipMalloc(reinterpret_cast<void **>(&x.slots), 3 * (size_t)KTH_STATS_WORDS * 8) != hipSuccess ||
@@ -199,7 +238,7 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
             break;
         }
     }
-    if (rc == KTH_OK) {
+    if (rc == KTH_OK && !local) {
         if (rccl().CommInitAll(comms.data(), ngpu, devices) != ncclSuccess)
             rc = KTH_ECOMM;
         else
@@ -212,6 +251,31 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
     }
     *out = h;
     return KTH_OK;
+}
+
+int64_t kth_sharded_sample_split(const int64_t *shard_n, int P, int64_t *s_dev) {
+    if (!shard_n || !s_dev || P < 1) return KTH_EINVAL;
+    int64_t n_total = 0;
+    for (int i = 0; i < P; ++i) {
+        if (shard_n[i] < 0) return KTH_EINVAL;
+        n_total += shard_n[i];
+    }
+    if (n_total < 1) return KTH_EINVAL;
+    // ~kth_dist_sample_size(n_total) sample keys in all, split over the shards
+    // in proportion to their sizes (a multiple of 64 each, at least 64, at
+    // most the shard rounded down to 64): the gathered sample is then ~uniform
+    // over the union also for unbalanced shards, so the window is as good a
+    // guess as one GPU's
+    const int64_t s_want = kth_dist_sample_size(n_total);
+    int64_t s_total = 0;
+    for (int i = 0; i < P; ++i) {
+        const double share = (double)s_want * (double)shard_n[i] / (double)n_total;
+        int64_t si = std::max<int64_t>(64, (int64_t)share & ~int64_t(63));
+        si = std::min<int64_t>(si, shard_n[i] & ~int64_t(63));
+        s_dev[i] = si;
+        s_total += si;
+    }
+    return s_total;
 }
 
 int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const int64_t *shard_n, int64_t k,
@@ -228,31 +292,34 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     if (n_min < SMALL_PER_GPU) return select_gathered(h, shards, shard_n, n_total, k, out);
     const auto t0 = std::chrono::steady_clock::now();
 
-    // ~kth_dist_sample_size(n_total) sample keys in all, split over the devices
-    // in proportion to their shard sizes (a multiple of 64 each, at least 64, at
-    // most the shard): the gathered sample is then ~uniform over the union also
-    // for unbalanced shards, so the window is as good a guess as one GPU's.
-    // Balanced shards give every device the same count and one all-gather;
-    // unequal counts are gathered as one group of broadcasts (a gatherv).
-    const int64_t s_want = kth_dist_sample_size(n_total);
+    // per-shard sample sizes (kth_sharded_sample_split); balanced shards give
+    // every shard the same count and one all-gather, unequal counts are
+    // gathered as one group of broadcasts (a gatherv) over RCCL
     std::vector<int64_t> s_dev((size_t)P), s_off((size_t)P + 1, 0);
+    const int64_t s_total = kth_sharded_sample_split(shard_n, P, s_dev.data());
+    TRY(s_total);
     bool equal = true;
     for (int i = 0; i < P; ++i) {
-        const double share = (double)s_want * (double)shard_n[i] / (double)n_total;
-        int64_t si = std::max<int64_t>(64, (int64_t)share & ~int64_t(63));
-        si = std::min<int64_t>(si, shard_n[i] & ~int64_t(63));
-        s_dev[(size_t)i] = si;
-        s_off[(size_t)i + 1] = s_off[(size_t)i] + si;
-        equal = equal && si == s_dev[0];
+        s_off[(size_t)i + 1] = s_off[(size_t)i] + s_dev[(size_t)i];
+        equal = equal && s_dev[(size_t)i] == s_dev[0];
     }
-    const int64_t s_total = s_off[(size_t)P];
     const Rccl &R = rccl();
-    for (int i = 0; i < P; ++i) {
-        Dev &x = h->d[(size_t)i];
-        TRY(grow(x.device, reinterpret_cast<void **>(&x.sample), &x.sample_cap, s_dev[(size_t)i] * 4));
-        TRY(grow(x.device, reinterpret_cast<void **>(&x.gathered), &x.gathered_cap, s_total * 4));
+    if (h->local) {
+        TRY(grow(h->d[0].device, reinterpret_cast<void **>(&h->lgathered), &h->lgathered_cap, s_total * 4));
+    } else {
+        for (int i = 0; i < P; ++i) {
+            Dev &x = h->d[(size_t)i];
+            TRY(grow(x.device, reinterpret_cast<void **>(&x.sample), &x.sample_cap, s_dev[(size_t)i] * 4));
+            TRY(grow(x.device, reinterpret_cast<void **>(&x.gathered), &x.gathered_cap, s_total * 4));
+        }
     }
+    std::vector<uint64_t *> slot_bufs((size_t)P);
+    for (int i = 0; i < P; ++i) slot_bufs[(size_t)i] = h->d[(size_t)i].slots;
     auto allreduce = [&](int slot) -> int {
+        if (h->local) {  // one stream: every shard's step is complete before the sum runs
+            HIPT(hipSetDevice(h->d[0].device));
+            return kth_internal_slots_sum(slot_bufs.data(), P, slot, h->d[0].stream);
+        }
         NCCLT(R.GroupStart());
         for (Dev &x : h->d) {
             uint64_t *p = x.slots + (size_t)slot * KTH_STATS_WORDS;
@@ -264,32 +331,39 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
         NCCLT(R.GroupEnd());
         return KTH_OK;
     };
+    // the samples: local -> straight into the shared gathered buffer at each
+    // shard's offset; RCCL -> the shard's buffer, then an all-gather (or a
+    // gatherv of broadcasts)
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];
+        uint32_t *dst = h->local ? h->lgathered + s_off[(size_t)i] : x.sample;
         TRY(kth_dist_begin(x.ctx, x.slots, n_total, k));
-        TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], x.sample, s_dev[(size_t)i]));
+        TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], dst, s_dev[(size_t)i]));
     }
-    NCCLT(R.GroupStart());
-    for (int i = 0; i < P; ++i) {
-        Dev &x = h->d[(size_t)i];
-        ncclResult_t r = ncclSuccess;
-        if (equal) {
-            r = R.AllGather(x.sample, x.gathered, (size_t)s_dev[0], ncclUint32, x.comm, x.stream);
-        } else {
-            for (int root = 0; root < P && r == ncclSuccess; ++root)
-                r = R.Broadcast(root == i ? x.sample : nullptr, x.gathered + s_off[(size_t)root],
-                                (size_t)s_dev[(size_t)root], ncclUint32, root, x.comm, x.stream);
+    if (!h->local) {
+        NCCLT(R.GroupStart());
+        for (int i = 0; i < P; ++i) {
+            Dev &x = h->d[(size_t)i];
+            ncclResult_t r = ncclSuccess;
+            if (equal) {
+                r = R.AllGather(x.sample, x.gathered, (size_t)s_dev[0], ncclUint32, x.comm, x.stream);
+            } else {
+                // (every rank passes its own sample as the send buffer; only the root's is read)
+                for (int root = 0; root < P && r == ncclSuccess; ++root)
+                    r = R.Broadcast(x.sample, x.gathered + s_off[(size_t)root], (size_t)s_dev[(size_t)root], ncclUint32,
+                                    root, x.comm, x.stream);
+            }
+            if (r != ncclSuccess) {
+                (void)R.GroupEnd();
+                return KTH_ECOMM;
+            }
         }
-        if (r != ncclSuccess) {
-            (void)R.GroupEnd();
-            return KTH_ECOMM;
-        }
+        NCCLT(R.GroupEnd());
     }
-    NCCLT(R.GroupEnd());
     int slot = -1;
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];
-        TRY(kth_dist_window(x.ctx, x.gathered, s_total));
+        TRY(kth_dist_window(x.ctx, h->local ? h->lgathered : x.gathered, s_total));
         const int r = kth_dist_scan(x.ctx, shards[i], shard_n[i]);
         TRY(r);
         slot = r;
@@ -305,8 +379,8 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     }
     for (Dev &x : h->d) TRY(kth_dist_result(x.ctx, x.out));
     h->enqueue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    // every device must hold the same answer (they picked the same digits from
-    // the same reduced histograms); the per-device error words must be clear
+    // every shard must hold the same answer (they picked the same digits from
+    // the same reduced histograms); the per-shard error words must be clear
     int32_t first = 0;
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];

@@ -25,6 +25,7 @@ import numpy as np
 from ._lib import (  # noqa: F401
     KTH_DIST_LEVELS,
     KTH_ECOMM,
+    KTH_EINTERNAL,
     KTH_EINVAL,
     KTH_ENODEV,
     KTH_OK,

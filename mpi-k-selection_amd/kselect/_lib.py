@@ -113,6 +113,7 @@ PROTOS = {
     "kth_sharded_select_i32": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_i32p]),
     "kth_select_i32_sharded": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int64, c_i32p]),
     "kth_sharded_enqueue_us": (ctypes.c_double, [c_vp]),
+    "kth_sharded_sample_split": (ctypes.c_int64, [c_vp, ctypes.c_int, c_vp]),
     # vector.h
     "VecNew": (IntVectorPtr, [ctypes.c_int]),
     "VecAdd": (ctypes.c_int, [IntVectorPtr, ctypes.c_int]),

@@ -29,7 +29,8 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import KTH_DIST_LEVELS, KTH_STATS_WORDS, LIB as _lib, Selector, check, check_single_runtime
+from . import KTH_DIST_LEVELS, KTH_EINTERNAL, KTH_STATS_WORDS, LIB as _lib, KthError, Selector, check, \
+    check_single_runtime
 from .rccl import RcclComm, TorchComm
 
 SMALL_PER_RANK = 64  # below this many keys per rank: all-gather and select locally
@@ -97,6 +98,10 @@ class HipBackend:
     def alloc_out(self):
         return torch.empty(1, dtype=torch.int32, device=self.device)
 
+    def error(self):
+        """The last selection's device error word (kth_ctx_last_stats; synchronises)."""
+        return int(self.sel.stats()["error"])
+
     def select_all(self, keys, n, k, out):
         """k-th smallest of keys[0..n) on this GPU (the small-input path)."""
         self.sel.select_async(keys, n, k, out)
@@ -105,11 +110,11 @@ class HipBackend:
 class DistSelector:
     """k-th smallest of the union of every rank's shard (global 1-based k)."""
 
-    def __init__(self, backend, group=None, comm=None):
+    def __init__(self, backend, group=None, comm=None, world=None):
         self.b = backend
         self.group = group
-        self.world = dist.get_world_size(group)
-        if comm is None:
+        self.world = dist.get_world_size(group) if world is None else int(world)
+        if comm is None and world is None:
             comm = backend.make_comm(group) if hasattr(backend, "make_comm") else TorchComm(group)
         self.comm = comm
         self.slots = backend.alloc_slots()
@@ -118,40 +123,72 @@ class DistSelector:
         self._gathered = None
         self._checked = None  # last (n_local, n_total, k) every rank agreed on
 
+    def s_local(self, n_total):
+        """Sample keys per rank: the window needs ~sample_size(n_total) keys in
+        all (what one GPU would take), not that many per rank, so the
+        all-gather stays ~4 MiB."""
+        return max(64, (self.b.sample_size(n_total) // self.world) & ~63)
+
+    def steps(self, shard, n_local, n_total, k, out):
+        """The per-rank protocol as a generator: the device steps run in the
+        generator, each collective is yielded to the caller, who performs it
+        across the ranks before resuming -- ("all_gather", dst, src) or
+        ("all_reduce", t), SUM in place (select() runs them over self.comm;
+        lockstep() performs them for P selectors in one process)."""
+        b = self.b
+        s_local = self.s_local(n_total)
+        if self._sample is None or self._sample.numel() != s_local:
+            self._sample = b.alloc_sample(s_local)
+            self._gathered = b.alloc_sample(s_local * self.world)
+        b.begin(self.slots, n_total, k)
+        b.sample(shard, n_local, self._sample, s_local)
+        yield ("all_gather", self._gathered, self._sample)
+        b.window(self._gathered, s_local * self.world)
+        i = b.scan(shard, n_local)
+        yield ("all_reduce", self.slots[i])
+        for level in range(KTH_DIST_LEVELS):
+            i = b.level(shard, n_local, level)
+            yield ("all_reduce", self.slots[i])
+        b.result(out)
+
     def select(self, shard, n_local, n_total, k, out=None):
         """Enqueue one selection; returns the device (or CPU, for gloo) int32[1]
         answer tensor (``out`` if given, else a buffer reused by every call).
+        Asynchronous: a device-side failure (e.g. a timed-out grid barrier)
+        leaves ``out`` unwritten -- ``error()`` / ``value()`` report it.
 
         n_total must be the sum of n_local over ranks and k in [1, n_total];
         every rank must pass the same (n_total, k).  Shards are expected to be
         balanced (every n_local >= n_total // world, as the block partition of
         shard_bounds gives); below SMALL_PER_RANK keys per rank the shards are
         all-gathered and every rank selects from the union."""
-        b = self.b
         out = self.out if out is None else out
         if n_total // self.world < SMALL_PER_RANK:
             if not (1 <= k <= n_total):
                 raise ValueError(f"k={k} outside [1, {n_total}]")
             return self._select_small(shard, n_local, n_total, k, out)
-        # the window needs ~sample_size(n_total) sample keys in all (what one GPU
-        # would take), not that many per rank: the all-gather stays ~4 MiB
-        s_local = max(64, (b.sample_size(n_total) // self.world) & ~63)
         if self._checked != (n_local, n_total, k):
-            self._check_args(n_local, n_total, k, s_local)
-        if self._sample is None or self._sample.numel() != s_local:
-            self._sample = b.alloc_sample(s_local)
-            self._gathered = b.alloc_sample(s_local * self.world)
-        b.begin(self.slots, n_total, k)
-        b.sample(shard, n_local, self._sample, s_local)
-        self.comm.all_gather(self._gathered, self._sample)
-        b.window(self._gathered, s_local * self.world)
-        i = b.scan(shard, n_local)
-        self.comm.all_reduce_sum_(self.slots[i])
-        for level in range(KTH_DIST_LEVELS):
-            i = b.level(shard, n_local, level)
-            self.comm.all_reduce_sum_(self.slots[i])
-        b.result(out)
+            self._check_args(n_local, n_total, k, self.s_local(n_total))
+        for op in self.steps(shard, n_local, n_total, k, out):
+            if op[0] == "all_gather":
+                self.comm.all_gather(op[1], op[2])
+            else:
+                self.comm.all_reduce_sum_(op[1])
         return out
+
+    def error(self):
+        """The device error word of this rank's last selection (0 = none;
+        synchronises).  A nonzero word means the answer tensor was NOT written."""
+        return self.b.error() if hasattr(self.b, "error") else 0
+
+    def value(self, shard, n_local, n_total, k):
+        """select() + wait: the answer as an int, KthError(KTH_EINTERNAL) when
+        the device reports an error (the answer buffer would hold a stale value)."""
+        out = self.select(shard, n_local, n_total, k)
+        err = self.error()
+        if err:
+            raise KthError(KTH_EINTERNAL, f"sharded select: device error {err}")
+        return int(out.item())
 
     def _check_args(self, n_local, n_total, k, s_local):
         """Validate the arguments across ranks (two small collectives, once per
@@ -194,3 +231,46 @@ class DistSelector:
 
     def close(self):
         self.comm.close()
+
+
+def lockstep(selectors, shards, n_locals, k, outs=None, observe=None):
+    """P selectors of one process, one shard each, run the protocol in
+    lockstep: every selector's steps up to its next collective, then the
+    collective performed here -- the all-gather as a concatenation of the P
+    samples, the all-reduce as the SUM of the P slots written back to each.
+    The Python mirror of kth_sharded's local transport (P shards on one
+    device; also P CPU backends in tests).  Returns the P answer tensors.
+    ``observe(kind, tensors)`` sees every collective's result."""
+    P = len(selectors)
+    if not (len(shards) == len(n_locals) == P) or P < 1:
+        raise ValueError("one shard and one size per selector")
+    n_total = int(sum(int(n) for n in n_locals))
+    if not (1 <= k <= n_total):
+        raise ValueError(f"k={k} outside [1, {n_total}]")
+    if any(s.world != P for s in selectors):
+        raise ValueError(f"selectors built for world {[s.world for s in selectors]}, lockstep runs {P}")
+    s_local = selectors[0].s_local(n_total)
+    if min(int(n) for n in n_locals) < s_local:
+        raise ValueError(f"some shard is smaller than the per-rank sample ({s_local} keys)")
+    outs = [s.out for s in selectors] if outs is None else outs
+    gens = [s.steps(sh, int(n), n_total, k, o) for s, sh, n, o in zip(selectors, shards, n_locals, outs)]
+    while True:
+        ops = [next(g, None) for g in gens]
+        if all(op is None for op in ops):
+            return outs
+        if any(op is None for op in ops) or len({op[0] for op in ops}) != 1:
+            raise RuntimeError(f"selectors out of step: {[op and op[0] for op in ops]}")
+        if ops[0][0] == "all_gather":
+            cat = torch.cat([op[2] for op in ops])
+            for op in ops:
+                op[1].copy_(cat)
+            res = cat
+        else:
+            total = ops[0][1].clone()
+            for op in ops[1:]:
+                total += op[1]
+            for op in ops:
+                op[1].copy_(total)
+            res = total
+        if observe:
+            observe(ops[0][0], res)

@@ -69,9 +69,13 @@ def test_sharded_errors(gpu, sharded):
     with pytest.raises(kselect.KthError) as e:  # host memory is not a shard
         kselect.select_sharded([np.zeros(1000, dtype=np.int32)], 5)
     assert e.value.code == kselect.KTH_EINVAL
-    with pytest.raises(kselect.KthError) as e:  # one rank per device
-        kselect.ShardedSelector([0, 0])
+    with pytest.raises(kselect.KthError) as e:  # the local transport holds at most 64 shards
+        kselect.ShardedSelector([0] * 65)
     assert e.value.code == kselect.KTH_EINVAL
+    if _ndev() >= 2:  # a device repeated among others: neither RCCL (one rank per device) nor local
+        with pytest.raises(kselect.KthError) as e:
+            kselect.ShardedSelector([0, 1, 0])
+        assert e.value.code == kselect.KTH_EINVAL
 
 
 @pytest.mark.parametrize("fam", FAMS)
