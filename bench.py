@@ -284,11 +284,15 @@ def rows_main(args):
     f32 = args.rows_dtype == "f32"
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + rank)
+    dup = args.rows_input == "dup"
     if f32:
         m = torch.rand((R, C), generator=g, device=dev, dtype=torch.float32) * 2 - 1
+        if dup:  # duplicate-heavy: 17 distinct values per row
+            m = torch.round(m * 8) / 8
         out = torch.empty(R, dtype=torch.float32, device=dev)
     else:
-        m = torch.randint(-2 ** 31, 2 ** 31, (R, C), generator=g, device=dev, dtype=torch.int64).to(torch.int32)
+        lo, hi = (-3, 4) if dup else (-2 ** 31, 2 ** 31)  # duplicate-heavy: 7 distinct values
+        m = torch.randint(lo, hi, (R, C), generator=g, device=dev, dtype=torch.int64).to(torch.int32)
         out = torch.empty(R, dtype=torch.int32, device=dev)
 
     if args.topk:
@@ -332,7 +336,7 @@ def rows_main(args):
     value = keys_total / (elapsed / args.steps) / 1e9
     achieved = 4.0 * R * C / (kern_ms * 1e-3) / 1e9
     rows_traffic, rows_note = None, "no PMC measurement for this workload"
-    if not args.topk and (R, C, k) == (65536, 4096, 64):
+    if not args.topk and not dup and (R, C, k) == (65536, 4096, 64):
         rows_traffic, rows_note = pmc_traffic(f"pmc_traffic_rows_{args.rows_dtype}.json", None, None)
     res = {
         "metric": ("Gkeys/s batched top-k (largest) per row" if args.topk else "Gkeys/s batched k-th per row")
@@ -340,9 +344,11 @@ def rows_main(args):
         "value": value, "unit": "Gkeys/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32" if f32 else "int32",
-        "data": "synthetic (torch.rand / torch.randint on device)",
+        "data": "synthetic (torch.rand / torch.randint on device)" + (
+            ", duplicate-heavy: f32 round(u*8)/8 (17 values), int32 randint[-3, 3] (7 values)" if dup else ""),
         "config": {"workload": f"{'top-k' if args.topk else 'k-th'} per row of a {R} x {C} "
-                               f"{'f32' if f32 else 'int32'} matrix, k={k}",
+                               f"{'f32' if f32 else 'int32'} matrix, k={k}" + (", duplicate-heavy" if dup else ""),
+                   "input": args.rows_input,
                    "rows": R, "cols": C, "k": k, "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "kth::k_rows_reg" if C <= 4096 else "kth::k_rows",
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -469,6 +475,8 @@ def main():
     ap.add_argument("--cols", type=int, default=4096)
     ap.add_argument("--rows-dtype", choices=["i32", "f32"], default="i32")
     ap.add_argument("--topk", action="store_true", help="rows workload: top-k (largest) values + columns per row")
+    ap.add_argument("--rows-input", choices=["uniform", "dup"], default="uniform",
+                    help="rows workload input: uniform (f32 U(-1,1), int32 full range) or dup (duplicate-heavy)")
     ap.add_argument("--probe-launch", action="store_true",
                     help="(tests) each rank prints its launch environment as JSON and exits before touching a GPU")
     args = ap.parse_args()

@@ -347,6 +347,95 @@ __device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
     return (uint32_t)__builtin_amdgcn_fmed3f(__builtin_fmaf(v, s, o), 0.f, 255.f);
 }
 
+// A picked bin of more than 64 keys (duplicate-heavy or clustered rows; was:
+// four masked 8-bit radix sweeps of the whole row, ~24-35 VALU ops and four
+// LDS atomics a key, and the atomics of a few-valued row serialise on a few
+// addresses).  b is monotone, so bin B's keys are exactly the order keys of
+// one interval [amin, amax] (min / max over the bin, one pass):
+//   amin == amax: one value (a value-linear float row with values spaced wider
+//       than a bin): it is the answer;
+//   amax - amin < 8: at most 8 values: every lane counts its keys of each
+//       value in 8-bit fields of two registers (no LDS atomics), one wave sum
+//       per pair of values in 16-bit fields, then the kk-th;
+//   wider (clustered rows): the masked radix sweeps of the whole row
+//       (row_select_radix, rank kk_row in the row).
+// kk is the rank within bin B on entry and within the answer's equal keys on
+// return; key[] holds order keys (xor flip) on return.
+template <bool F32, int KPL, typename ToKeys>
+__device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
+                                                         uint32_t kk_row, uint32_t flip, bool vmap, float fs, float fo,
+                                                         uint32_t bin, uint32_t cnt, uint32_t *eq_out,
+                                                         ToKeys &&to_keys) {
+    uint32_t amin = 0xFFFFFFFFu, amax = 0u;
+    if (F32 && vmap) {  // key[] holds raw float bits: the bin test on the value, min / max on the order key
+        const float s2 = opaque(fs);
+        float o2;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
+        const uint32_t ob = opaque(bin), fl = opaque(flip);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const bool in = vbin(__uint_as_float(key[j]), s2, o2) == ob;
+            const uint32_t u = key_of_f32(key[j]) ^ fl;
+            amin = in ? min(amin, u) : amin;
+            amax = in ? max(amax, u) : amax;
+        }
+        to_keys();
+    } else {
+        const uint32_t ob = opaque(bin);
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const bool in = (key[j] >> 24) == ob;
+            amin = in ? min(amin, key[j]) : amin;
+            amax = in ? max(amax, key[j]) : amax;
+        }
+    }
+    amin = wave_min_u32(amin);
+    amax = wave_max_u32(amax);
+    const uint32_t span = amax - amin;
+    if (span == 0) {
+        if (eq_out) *eq_out = cnt;
+        return amin;
+    }
+    if (span < 8) {
+        // value d = x - amin of every key in [amin, amax]: field d & 3 of c[d >> 2]
+        const uint32_t ob = opaque(amin);
+        uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const uint32_t d = key[j] - ob;
+            const uint32_t inc = 1u << ((d & 3u) << 3);
+            c0 += d < 4u ? inc : 0u;
+            c1 += d - 4u < 4u ? inc : 0u;
+        }
+        // (a lane counts <= KPL <= 64 keys a value: 8-bit fields; the wave sums in 16-bit fields)
+        const auto add = [](uint32_t a, uint32_t b) { return a + b; };
+        const uint32_t s01 = wave_reduce(c0 & 0x00FF00FFu, 0u, add), s23 = wave_reduce((c0 >> 8) & 0x00FF00FFu, 0u, add);
+        const uint32_t s45 = wave_reduce(c1 & 0x00FF00FFu, 0u, add), s67 = wave_reduce((c1 >> 8) & 0x00FF00FFu, 0u, add);
+        const uint32_t n[8] = {s01 & 0xFFFFu, s23 & 0xFFFFu, s01 >> 16, s23 >> 16,
+                               s45 & 0xFFFFu, s67 & 0xFFFFu, s45 >> 16, s67 >> 16};
+        uint32_t d = 0, acc = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (acc < kk) {  // wave-uniform
+                d = (uint32_t)q;
+                acc += n[q];
+            }
+        kk -= acc - n[d];
+        if (eq_out) *eq_out = n[d];
+        return amin + d;
+    }
+    // wider intervals (clustered rows; rare): the masked radix sweeps of the row
+    const uint32_t ans = row_select_radix<KPL, 4>(key, hist, lane, kk_row);
+    kk = kk_row;
+    if (eq_out) {
+        uint32_t e = 0;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) e += key[j] == ans ? 1u : 0u;
+        *eq_out = wave_reduce(e, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+    }
+    return ans;
+}
+
 // Fast path for full rows (cols = 64 * KPL, 16-byte aligned): one histogram
 // pass, then the keys of the picked bin go to an LDS list and are ranked there.
 //   pass A: 256 bins of a monotone map b(x) -- the top byte of the order key
@@ -362,7 +451,7 @@ __device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
 // b is monotone, so the bin's keys are exactly the keys between two order
 // keys, and the kk-th of the row is the kk-th (after the keys below B) of the
 // list.  A bin of more than 64 keys (duplicate-heavy or clustered rows) goes
-// to the masked radix sweeps of row_select_radix.  On return key[] holds order
+// to row_select_dense_bin.  On return key[] holds order
 // keys (xor flip) when KEYS_OUT (top-k compaction); else float rows may keep
 // raw bits.  *eq_out: how many keys of the row equal the answer.
 // Top-k rows (STAGE): the filter pass also stages every key of the bins up to
@@ -444,15 +533,9 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     wave_pick(hist, R0, lane, kk, bin, below, cnt);
     __builtin_amdgcn_wave_barrier();  // every lane's histogram reads before the list overwrites it
     if (cnt > (uint32_t)WAVE) {
-        if (F32 && vmap) to_keys();
-        const uint32_t ans = row_select_radix<KPL, R0>(key, hist, lane, kk);
-        if (eq_out) {
-            uint32_t e = 0;
-#pragma unroll
-            for (int j = 0; j < KPL; ++j) e += key[j] == ans ? 1u : 0u;
-            *eq_out = wave_reduce(e, 0u, [](uint32_t a, uint32_t b) { return a + b; });
-        }
-        return ans;
+        kk -= below;
+        return row_select_dense_bin<F32, KPL>(key, hist, lane, kk, kk + below, flip, vmap, fs, fo, bin, cnt, eq_out,
+                                              to_keys);
     }
     kk -= below;
 

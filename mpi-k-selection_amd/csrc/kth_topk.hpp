@@ -373,26 +373,6 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
 // whose entries are the wave's wave-rows' staged keys back to back in that
 // order (row words: counts).  Lane l takes one wave-row of each window of 64.
 
-// The entries of one wave-row, e in [0, c), four loads in flight per lane
-// (a rolled per-entry loop waited one memory round trip per entry); with sp,
-// their positions are loaded beside them (f(x, p)).
-template <typename F>
-__device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
-                                            uint32_t c, F &&f) {
-    for (uint32_t e0 = 0; e0 < c; e0 += 4) {
-        int32_t x[4];
-        uint8_t p[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            x[q] = e0 + q < c ? sv[e0 + q] : 0;
-            if (sp) p[q] = e0 + q < c ? sp[e0 + q] : (uint8_t)0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (e0 + q < c) f(x[q], p[q]);
-    }
-}
-
 // The staged kernels' split: gridDim.x = G * S workgroups; workgroup
 // (b, part) takes part `part` of the windows of k_main's workgroup b (its
 // waves' segments), each window starting at the entry offsets k_main<5/6>
@@ -415,6 +395,63 @@ __device__ __forceinline__ uint32_t tk5_wstart(const uint32_t *wstart, uint32_t 
     return win == 0 ? 0u : wstart[(b * (TK_BLOCK / WAVE) + (u64)w) * nwin + win];
 }
 
+// The entries of one wave-row, e in [0, c), KTH_TK5_BATCH loads in flight per
+// lane (a rolled per-entry loop waited one memory round trip per entry; 4 in
+// flight: one round trip per 4 entries); with sp, their positions are loaded
+// beside them (f(x, p)).
+#ifndef KTH_TK5_BATCH
+#define KTH_TK5_BATCH 16
+#endif
+#ifndef KTH_TK5_CHUNKED  // 1: the window's entries staged in LDS by coalesced chunks (A/B)
+#define KTH_TK5_CHUNKED 0
+#endif
+template <typename F>
+__device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
+                                            uint32_t c, F &&f) {
+    constexpr int B = KTH_TK5_BATCH;
+    for (uint32_t e0 = 0; e0 < c; e0 += B) {
+        int32_t x[B];
+        uint8_t p[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            x[q] = e0 + q < c ? sv[e0 + q] : 0;
+            p[q] = sp && e0 + q < c ? sp[e0 + q] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+            if (e0 + q < c) f(x[q], p[q]);
+    }
+}
+
+// A window's entries (the 64 wave-rows' staged keys, back to back from the
+// window's first entry ws0) are brought into the wave's LDS in chunks of
+// TK5_ECHUNK with coalesced loads, all of a lane's loads in flight at once
+// (a lane walking its own wave-row's entries waited one memory round trip
+// per few entries: k_tk5_count 165 us, k_tk5_write 394 us at k = 2^26).  Lane
+// l then walks its wave-row's part of each chunk, [s0, s1) of the window,
+// from LDS.  f(e, x) stages entry e (window-relative) of value x.
+constexpr int TK5_ECHUNK = 1024;  // entries per wave and chunk
+__device__ __forceinline__ uint32_t tk5_clip(uint32_t e, uint32_t c0, uint32_t cn) {  // window entry e in chunk [c0, c0 + cn)
+    return e <= c0 ? 0u : (e - c0 < cn ? e - c0 : cn);
+}
+template <typename T, typename F>
+__device__ __forceinline__ void tk5_chunk_load(const T *__restrict__ sv, uint32_t ws0, uint32_t c0, uint32_t cn,
+                                               F &&f) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    constexpr int PER = TK5_ECHUNK / WAVE;
+    T x[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t e = (uint32_t)(q * WAVE + lane);
+        x[q] = e < cn ? sv[ws0 + c0 + e] : (T)0;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t e = (uint32_t)(q * WAVE + lane);
+        if (e < cn) f(e, x[q]);
+    }
+}
+
 // Per wave-row: #better | #equal << 16 -> wcnt; per row (the 4 wave-rows of
 // its 4 waves, summed through LDS) -> tcnt.  Entries are read, the input is not.
 __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restrict__ segv, u64 seg_cap,
@@ -423,24 +460,46 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
                                                         const int32_t *__restrict__ d_v, uint32_t flip,
                                                         uint32_t *__restrict__ wcnt, uint32_t *__restrict__ tcnt) {
     __shared__ uint32_t part[TK_BLOCK / WAVE][WAVE];
+#if KTH_TK5_CHUNKED
+    __shared__ uint32_t ecode[TK_BLOCK / WAVE][TK5_ECHUNK];  // an entry's #better | #equal << 16
+#endif
     if (!tk5_ok(tflags, d_v)) return;  // grid-uniform
     const int32_t v = d_v[0];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const Tk5Part P = tk5_part(nfull, G);
     const int32_t *sv = segv + (P.b * (TK_BLOCK / WAVE) + w) * seg_cap;
     const uint32_t *ws = tflags + TF_W0 + (P.b * (TK_BLOCK / WAVE) + w) * rw_seg_words(nfull, G);  // this wave's row words
+#if KTH_TK5_CHUNKED
+    uint32_t *ec = ecode[w];
+#endif
     for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
         const u64 j = win * WAVE + lane;
         const bool valid = j < P.m;
         const u64 r = (P.b + (j / MAIN_UNROLL) * P.G) * MAIN_UNROLL + j % MAIN_UNROLL;
         const uint32_t c = valid ? ws[j] : 0u;
-        const uint32_t start = tk5_wstart(wstart, nwin, P.b, w, win) + wave_incl_scan32(c) - c;
+        const uint32_t incl = wave_incl_scan32(c), s0 = incl - c;
+#if !KTH_TK5_CHUNKED
         uint32_t nb = 0, ne = 0;
-        tk5_entries(sv + start, nullptr, c, [&](int32_t x, uint8_t) {
+        tk5_entries(sv + tk5_wstart(wstart, nwin, P.b, w, win) + s0, nullptr, c, [&](int32_t x, uint8_t) {
             nb += (flip == 0u ? x < v : x > v) ? 1u : 0u;
             ne += x == v ? 1u : 0u;
         });
         const uint32_t word = nb | ne << 16;
+#else
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);  // the window's entries
+        const uint32_t ws0 = tk5_wstart(wstart, nwin, P.b, w, win);
+        uint32_t word = 0;
+        for (uint32_t c0 = 0; c0 < T; c0 += TK5_ECHUNK) {  // wave-uniform
+            const uint32_t cn = T - c0 < (uint32_t)TK5_ECHUNK ? T - c0 : (uint32_t)TK5_ECHUNK;
+            tk5_chunk_load(sv, ws0, c0, cn, [&](uint32_t e, int32_t x) {
+                ec[e] = ((flip == 0u ? x < v : x > v) ? 1u : 0u) | (x == v ? 0x10000u : 0u);
+            });
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t lo = tk5_clip(s0, c0, cn), hi = tk5_clip(incl, c0, cn);
+            for (uint32_t e = lo; e < hi; ++e) word += ec[e];
+            __builtin_amdgcn_wave_barrier();  // the chunk's LDS is rewritten next
+        }
+#endif
         if (valid) wcnt[r * (TK_BLOCK / WAVE) + w] = word;
         part[w][lane] = word;
         __syncthreads();
@@ -499,6 +558,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
     __shared__ uint16_t s_loc[TK5_STAGE];  // key index within its tile: u << 10 | w << 8 | position
     __shared__ u64 s_lo[8];                // tile i of the window: its first output slot
     __shared__ uint32_t s_off[9];          // and its first stage entry (s_off[8]: the window's total)
+#if KTH_TK5_CHUNKED
+    __shared__ int32_t e_val[TK_BLOCK / WAVE][TK5_ECHUNK];  // a chunk of each wave's window entries
+    __shared__ uint8_t e_pos[TK_BLOCK / WAVE][TK5_ECHUNK];
+#endif
     if (!tk5_ok(tflags, d_v) || meta[1]) return;  // grid-uniform
     const u64 need = meta[0];
     const int32_t v = d_v[0];
@@ -523,7 +586,8 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
         const Tk5Rec cur = nx;
         if (win + 1 < P.w_hi) nx = tk5_rec(ws, wcnt, tcnt, toff, bbase, row_of(j + WAVE), j + WAVE, j + WAVE < m);
         const uint32_t c = cur.c;
-        const uint32_t start = tk5_wstart(wstart, nwin, b, w, win) + wave_incl_scan32(c) - c;
+        const uint32_t wbase = tk5_wstart(wstart, nwin, b, w, win);  // the window's first entry
+        const uint32_t start = wbase + wave_incl_scan32(c) - c;
         // this row's bases, and this wave-row's (after the earlier quarters' counts)
         const u64 rb = cur.b0 + (cur.off & 0xFFFFFFFFull), re = cur.b1 + (cur.off >> 32);
         u64 bb = rb, be = re;
@@ -552,7 +616,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
         const bool staged = total <= (uint32_t)TK5_STAGE;  // block-uniform
         const uint16_t loc0 = (uint16_t)((lane & 7) << 10 | w << 8);
         const u64 i0 = r * TK_TILE + (u64)w * (TK_TILE / (TK_BLOCK / WAVE));  // the wave-row's first key
-        tk5_entries(segv + sbase + start, segp + sbase + start, c, [&](int32_t x, uint8_t p) {
+        auto place = [&](int32_t x, uint8_t p) __attribute__((always_inline)) {
             // (selects, not branches: with ++bb / ++be in branches the compiler
             // kept the pair in scratch and incremented it through a pointer)
             const bool isb = flip == 0u ? x < v : x > v, ise = x == v;
@@ -570,7 +634,24 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
                     if (idx) idx[pos] = (int64_t)(i0 + p);
                 }
             }
-        });
+        };
+#if !KTH_TK5_CHUNKED
+        tk5_entries(segv + sbase + start, segp + sbase + start, c, place);
+#else
+        const uint32_t incl = start - wbase + c, s0 = incl - c;  // this lane's entries in the window: [s0, incl)
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        int32_t *evw = e_val[w];
+        uint8_t *epw = e_pos[w];
+        for (uint32_t c0 = 0; c0 < T; c0 += TK5_ECHUNK) {  // wave-uniform
+            const uint32_t cn = T - c0 < (uint32_t)TK5_ECHUNK ? T - c0 : (uint32_t)TK5_ECHUNK;
+            tk5_chunk_load(segv + sbase, wbase, c0, cn, [&](uint32_t e, int32_t x) { evw[e] = x; });
+            tk5_chunk_load(segp + sbase, wbase, c0, cn, [&](uint32_t e, uint8_t x) { epw[e] = x; });
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t lo = tk5_clip(s0, c0, cn), hi = tk5_clip(incl, c0, cn);
+            for (uint32_t e = lo; e < hi; ++e) place(evw[e], epw[e]);
+            __builtin_amdgcn_wave_barrier();  // the chunk's LDS is rewritten next
+        }
+#endif
         if (staged) {  // coalesced copy-out, tile by tile
             __syncthreads();
             const u64 tile0 = (b + (j0 / MAIN_UNROLL) * G) * MAIN_UNROLL * TK_TILE;  // the window's first tile's first key

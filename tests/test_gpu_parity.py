@@ -389,6 +389,75 @@ def test_rows_i32_ranges(gpu, cols):
         np.testing.assert_array_equal(out.cpu().numpy(), _row_ref(m, k), err_msg=f"k={k}")
 
 
+def _dense_bin_rows(rng, rows, cols, f32):
+    """Rows whose picked first-pass bin holds more than 64 keys (the fast path's
+    row_select_dense_bin): one value per bin (span 0), at most 8 values in the
+    bin (per-lane register counts), and wider clusters (the radix sweeps) --
+    BASELINE config 5's duplicate-heavy variant and its neighbours."""
+    m = np.empty((rows, cols), dtype=np.float32 if f32 else np.int32)
+    for i in range(rows):
+        f = i % 6
+        if f32:
+            if f == 0:
+                m[i] = np.round(rng.uniform(-1, 1, cols) * 8) / 8          # 17 values, one per bin
+            elif f == 1:
+                m[i] = np.float32(1.0) + rng.integers(0, 8, cols) * np.float32(2 ** -23)  # 8 adjacent keys
+            elif f == 2:
+                m[i] = rng.choice(np.array([-1.5, 0.25, 3.0], dtype=np.float32), cols)
+            elif f == 3:
+                m[i] = np.where(rng.random(cols) < 0.5, rng.uniform(-1, 1, cols),
+                                np.float32(0.5) + rng.integers(0, 300, cols) * np.float32(2 ** -22))
+            elif f == 4:
+                m[i] = np.round(rng.normal(0, 1, cols) * 4) / 4
+            else:
+                m[i] = rng.uniform(-1, 1, cols)
+        else:
+            if f == 0:
+                m[i] = rng.integers(-3, 4, cols)                                # 7 values around 0
+            elif f == 1:
+                m[i] = (rng.integers(0, 16, cols) << 24) - 2 ** 31              # one value per top byte
+            elif f == 2:
+                m[i] = rng.integers(100, 108, cols)                             # 8 adjacent values
+            elif f == 3:
+                m[i] = rng.integers(0, 1000, cols)                              # a wide cluster (radix)
+            elif f == 4:
+                m[i] = np.where(rng.random(cols) < 0.3, 77, rng.integers(-2 ** 31, 2 ** 31, cols))
+            else:
+                m[i] = rng.integers(-2 ** 31, 2 ** 31, cols)
+    return m
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_rows_dense_bins(gpu, f32):
+    import torch
+    rows, cols = 240, 4096
+    rng = np.random.default_rng(1234 + f32)
+    m = _dense_bin_rows(rng, rows, cols, f32)
+    d = torch.from_numpy(m).cuda()
+    out = torch.empty(rows, dtype=torch.float32 if f32 else torch.int32, device="cuda")
+    keys = _f32_order_key(m).astype(np.int64) if f32 else m.astype(np.int64)
+    for k in (1, 2, 64, 1000, 2048, 4095, 4096):
+        gpu.rows(d, rows, cols, k, out, f32=f32)
+        gpu.sync()
+        idx = np.argsort(keys, axis=1, kind="stable")[:, k - 1]
+        want = m[np.arange(rows), idx]
+        got = out.cpu().numpy()
+        if f32:
+            np.testing.assert_array_equal(_f32_order_key(got), _f32_order_key(want), err_msg=f"k={k}")
+        else:
+            np.testing.assert_array_equal(got, want, err_msg=f"k={k}")
+    for k in (1, 64, 2048, 4096):
+        for largest in (False, True):
+            vals = torch.empty((rows, k), dtype=out.dtype, device="cuda")
+            idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+            gpu.topk_rows(d, rows, cols, k, vals, idx, largest=largest, f32=f32)
+            gpu.sync()
+            want_idx = _topk_ref(keys, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want_idx, err_msg=f"topk k={k} largest={largest}")
+            np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32),
+                                          np.take_along_axis(m, want_idx, axis=1).view(np.uint32))
+
+
 # ------------------------------------------------------------- top-k rows
 def _topk_ref(keys, k, largest):
     """Column-order top-k with ties by column: numpy restatement of the contract

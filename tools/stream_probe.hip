@@ -3,10 +3,15 @@
 //   read_sum<U,NT>   : 16-B loads, U loads in flight per thread, NT = nontemporal
 //   read_cmp<U,NT>   : the k_main per-key work without compaction (3 counters)
 //   read_ballot<U>   : + the per-key ballot the candidate compaction needs
-// Usage: stream_probe [log2n=30]
+// Usage: stream_probe [log2n=30] [bump]
+//   bump: after a 2 s idle pause, 40 back-to-back read_sum<8,nt> passes, each
+//   timed by events (is the select's slowdown a few passes after an idle
+//   start the device's, or ours?)
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -103,6 +108,16 @@ __global__ __launch_bounds__(256) void read_ballot(const u32x4 *__restrict__ v, 
     if (a + b + c == 0x12345678u || lbuf[lcount & 4095] == 0x12345678u) out[0] = a;
 }
 
+__global__ void fill_random(unsigned *p, unsigned long long n) {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        unsigned long long z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = (unsigned)((z ^ (z >> 31)) >> 32);
+    }
+}
+
 template <typename K, typename... A>
 float timeit(K kern, int grid, int reps, A... args) {
     hipEvent_t e0, e1;
@@ -133,6 +148,33 @@ int main(int argc, char **argv) {
     unsigned lo = 0xbc3c3c3cu - 1, hi = 0xbc3c3c3cu + 1;  // all keys "inside": worst case for ballots
     unsigned lo0 = 0x10u, hi0 = 0x20u;                      // no keys inside
     const double gb = n * 4.0 / 1e9;
+    if (argc > 2 && !strcmp(argv[2], "bump")) {
+        // random keys (a constant fill toggles no bits: less power than real data)
+        hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, reinterpret_cast<unsigned *>(v), n);
+        CK(hipDeviceSynchronize());
+        const unsigned wlo = 0x7F000000u, whi = 0x7F000000u + (1u << 24);  // ~0.4 % of random keys inside
+        for (int kind = 0; kind < 3; ++kind) {
+            sleep(2);
+            hipEvent_t ev[41];
+            for (auto &evt : ev) CK(hipEventCreate(&evt));
+            CK(hipEventRecord(ev[0]));
+            for (int i = 0; i < 40; ++i) {
+                if (kind == 0) hipLaunchKernelGGL((read_sum<8, true>), dim3(1024), dim3(256), 0, 0, v, nv, o);
+                else if (kind == 1) hipLaunchKernelGGL((read_cmp<4, true>), dim3(1024), dim3(256), 0, 0, v, nv, wlo, whi, o2);
+                else hipLaunchKernelGGL((read_ballot<4, true>), dim3(1024), dim3(256), 0, 0, v, nv, wlo, whi, o2);
+                CK(hipEventRecord(ev[i + 1]));
+            }
+            CK(hipEventSynchronize(ev[40]));
+            printf("bump %s ms:", kind == 0 ? "read_sum" : kind == 1 ? "read_cmp" : "read_ballot");
+            for (int i = 0; i < 40; ++i) {
+                float ms;
+                CK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+                printf(" %.3f", ms);
+            }
+            printf("\n");
+        }
+        return 0;
+    }
     int grids[] = {1024, 2048, 4096, 8192};
     for (int g : grids) {
         printf("grid %5d  sum U1 %6.0f  U2 %6.0f  U4 %6.0f  U8 %6.0f | nt U2 %6.0f  U4 %6.0f  U8 %6.0f GB/s\n", g,
