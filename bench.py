@@ -363,7 +363,7 @@ def rows_main(args):
     return 0 if verified else 1
 
 
-def pmc_traffic(name, log2n, family):
+def pmc_traffic(name, log2n, family, field="hbm_bytes_per_launch"):
     """HBM bytes per launch of the dominant kernel from profiles/<name> (two
     rocprofv3 --pmc passes, tools/pmc_traffic.py), used only when it was
     measured on the libkth.so build loaded now (kth_build_id) and on this
@@ -379,7 +379,7 @@ def pmc_traffic(name, log2n, family):
         return None, f"profiles/{name} was measured on libkth build {tj.get('build_id')}, loaded build is {here}"
     if log2n is not None and (tj.get("log2n"), tj.get("family")) != (log2n, family):
         return None, f"profiles/{name} is for 2^{tj.get('log2n')} {tj.get('family')}, not this workload"
-    return tj.get("hbm_bytes_per_launch"), f"profiles/{name} (PMC FETCH_SIZE/WRITE_SIZE, build {here})"
+    return tj.get(field), f"profiles/{name} (PMC FETCH_SIZE/WRITE_SIZE, build {here}; {tj.get('correction', '')})"
 
 
 def topk_main(args):
@@ -432,6 +432,8 @@ def topk_main(args):
                     and bool((idx[1:] > idx[:-1]).all()))
     # algorithmic bytes: the input read once + the k (value, int64 index) pairs written
     alg_bytes = 4 * n + 12 * k
+    traffic, traffic_note = pmc_traffic(f"pmc_traffic_topk_k{k}.json", args.log2n, args.family,
+                                        field="hbm_bytes_per_call")
     achieved = alg_bytes / (call_ms * 1e-3) / 1e9
     res = {
         "metric": "Gkeys/s top-k (smallest, values + int64 indices) of one int32 array",
@@ -443,7 +445,8 @@ def topk_main(args):
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "whole kth_topk_i32 call (select + count + scan + write)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": call_ms},
+                     "traffic": traffic, "traffic_source": traffic_note,
+                     "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": call_ms},
         "verified": verified,
     }
     if rank == 0:

@@ -110,8 +110,10 @@ int kth_ctx_enable_timing(kth_ctx *ctx, int on);
 int kth_ctx_take_timing(kth_ctx *ctx, int64_t *n_selects, double *main_ms, double *total_ms);
 
 /* --- batched rows (BASELINE config 5; no reference counterpart) -------------
- * out[r] = k-th smallest of row r of a rows x cols row-major matrix; one
- * workgroup per row, row resident in LDS.  1 <= cols <= KTH_ROWS_MAX_COLS.
+ * out[r] = k-th smallest of row r of a rows x cols row-major matrix.  cols <=
+ * 4096: one wavefront per row, the row held in the wave's registers (64 keys a
+ * lane at most); wider rows: one workgroup per row, the row resident in LDS.
+ * 1 <= cols <= KTH_ROWS_MAX_COLS.
  * float32 order: IEEE total order with -0.0 < +0.0 and every NaN last
  * (a NaN answer is returned as the canonical quiet NaN 0x7FC00000). */
 #define KTH_ROWS_MAX_COLS 16384

@@ -1019,6 +1019,7 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         // input-reading path (exact)
         const u64 seg_total = std::max<u64>({1ull << 20, (u64)n / 16, (u64)k + (u64)k / 8 + (u64)n / 64});
         seg_cap = c->topk_seg_cap ? c->topk_seg_cap : (seg_total + nwaves - 1) / nwaves;
+        seg_cap = (seg_cap + 3) & ~3ull;  // segments start 16-byte aligned (k_main<5/6> stores 4 entries a lane)
         KTH_TRY(reserve_cand(c, n));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segv), &c->tk_segv_cap, seg_cap * nwaves * 4));
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_segp), &c->tk_segp_cap, seg_cap * nwaves));

@@ -675,29 +675,43 @@ struct OrdStager {
     uint32_t *cand_out;
     TkSeg seg;
 
-    __device__ __forceinline__ void flush() {
+    // The region's entries to the wave's segment, as 16-byte key stores and
+    // 4-byte position stores (the segment is 16-byte aligned and a mid-pass
+    // flush writes a multiple of 4 entries: the 0-3 left over move to the
+    // region's front; `last` writes them too), and the flushed entries'
+    // candidates (lo < x < hi) to the candidate buffer.
+    __device__ __forceinline__ void flush(bool last = false) {
         const int lane = threadIdx.x & (WAVE - 1);
         __builtin_amdgcn_wave_barrier();
-        const uint8_t *pb = reinterpret_cast<const uint8_t *>(reg + CAP);
-        const u64 base = seg_base + seg_fill;
-        for (uint32_t i = lane; i < wfill; i += WAVE)
-            if (seg_fill + i < seg.cap) {
-                seg.vals[base + i] = (int32_t)reg[i];
-                seg.pos[base + i] = pb[i];
+        uint8_t *pb = reinterpret_cast<uint8_t *>(reg + CAP);
+        const uint32_t n4 = wfill & ~3u, nw = last ? wfill : n4;  // entries written now
+        const u64 base = seg_base + seg_fill;                     // a multiple of 4
+#ifndef KTH_DIAG_TK5_NOSEGSTORE  // diagnostic builds only (wrong top-k results): cost of the segment stores
+        const uint32_t room = seg_fill < seg.cap ? seg.cap - seg_fill : 0u;  // entries the segment still holds
+        for (uint32_t q = lane; 4 * q < n4; q += WAVE)
+            if (4 * q + 4 <= room) {
+                *reinterpret_cast<uint4 *>(seg.vals + base + 4 * q) = reinterpret_cast<const uint4 *>(reg)[q];
+                *reinterpret_cast<uint32_t *>(seg.pos + base + 4 * q) = reinterpret_cast<const uint32_t *>(pb)[q];
             }
-        if (seg_fill + wfill > seg.cap && lane == 0) *seg.ovf = 1u;
+        if (last && (uint32_t)lane < wfill - n4 && n4 + lane < room) {  // the last 0-3 entries
+            seg.vals[base + n4 + lane] = (int32_t)reg[n4 + lane];
+            seg.pos[base + n4 + lane] = pb[n4 + lane];
+        }
+#endif
+        if (seg_fill + nw > seg.cap && lane == 0) *seg.ovf = 1u;
         // the window's candidates -> the candidate buffer (one reservation)
         uint32_t nin = 0;
-        for (uint32_t i0 = 0; i0 < wfill; i0 += WAVE) {
-            const int32_t x = (int32_t)reg[(i0 + lane) < wfill ? i0 + lane : 0];
-            nin += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(i0 + lane < wfill && x > slo && x < shi));
+#ifndef KTH_DIAG_TK5_NOCANDS  // diagnostic builds only (wrong results): cost of the candidate filter
+        for (uint32_t i0 = 0; i0 < nw; i0 += WAVE) {
+            const int32_t x = (int32_t)reg[(i0 + lane) < nw ? i0 + lane : 0];
+            nin += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(i0 + lane < nw && x > slo && x < shi));
         }
         if (nin) {
             const u64 g = reserve_cands(cand_count, acc, cap, nin);
             uint32_t o = 0;
-            for (uint32_t i0 = 0; i0 < wfill; i0 += WAVE) {
-                const int32_t x = (int32_t)reg[(i0 + lane) < wfill ? i0 + lane : 0];
-                const bool in = i0 + lane < wfill && x > slo && x < shi;
+            for (uint32_t i0 = 0; i0 < nw; i0 += WAVE) {
+                const int32_t x = (int32_t)reg[(i0 + lane) < nw ? i0 + lane : 0];
+                const bool in = i0 + lane < nw && x > slo && x < shi;
                 const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
                 const uint32_t below =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
@@ -706,8 +720,22 @@ struct OrdStager {
             }
             winside += nin;
         }
-        seg_fill += wfill;
-        wfill = 0;
+#endif
+        // the 0-3 entries not written move to the front (read before any write: one wave, in order)
+        const uint32_t left = wfill - nw;
+        uint32_t kx = 0;
+        uint8_t px = 0;
+        if ((uint32_t)lane < left) {
+            kx = reg[nw + lane];
+            px = pb[nw + lane];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if ((uint32_t)lane < left) {
+            reg[lane] = kx;
+            pb[lane] = px;
+        }
+        seg_fill += nw;
+        wfill = left;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -869,7 +897,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
-    __shared__ uint32_t region[BLK / WAVE][WREG];
+    __shared__ __attribute__((aligned(16))) uint32_t region[BLK / WAVE][WREG];
     __shared__ u64 red[6][BLK / WAVE];
     __shared__ uint32_t rowx[BLK / WAVE][4];  // k_main<3/4>: a wave's row sums in transit
     KTH_STAMP(a, 0);
@@ -1106,6 +1134,11 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 seg.wstart[((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.nwin + w0 + lane] = wsr;
         }
     }
+    // TF 5 / 6: the wave's last entries (and its candidates, reserved by the
+    // wave); its LDS region is then free for the ragged keys below, which are
+    // outside k_main's full tiles (the top-k reads those rows from the input):
+    // they only count and go to the candidates, like the plain pass's keys
+    if constexpr (ORD) os.flush(true);
     // ragged end: the last partial tile, as masked groups of one workgroup
     const u64 rem0 = nfull * tile;
     if (blockIdx.x == (uint32_t)(nfull % gridDim.x))
@@ -1123,24 +1156,13 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
                 kk[4 * u + 3] = x.w;
                 ok |= in ? (0xFu << (4 * u)) : 0u;
             }
-            if constexpr (ORD) {  // (rows past k_main's full tiles: staged for the candidates only)
-#pragma unroll
-                for (int u = 0; u < S; ++u)
-                    (void)ord_keys(make_uint4(kk[4 * u], kk[4 * u + 1], kk[4 * u + 2], kk[4 * u + 3]), (ok >> (4 * u)) & 0xFu,
-                                   0u);
-            } else {
-                scan_keys<K, false>(kk, ok, slo, shi, clt, ceqlo, ceqhi, st);
-            }
+            scan_keys<K, false>(kk, ok, slo, shi, clt, ceqlo, ceqhi, st);
         }
     if (blockIdx.x == 0) {  // the < 4-key unaligned head and tail
         const bool okh = threadIdx.x < head, okt = threadIdx.x < n - tail0;
         const uint32_t kk[2] = {okh ? p[threadIdx.x] : 0u, okt ? p[tail0 + threadIdx.x] : 0u};
-        if constexpr (ORD)
-            (void)ord_keys(make_uint4(kk[0], kk[1], 0u, 0u), (okh ? 1u : 0u) | (okt ? 2u : 0u), 0u);
-        else
-            scan_keys<2, false>(kk, (okh ? 1u : 0u) | (okt ? 2u : 0u), slo, shi, clt, ceqlo, ceqhi, st);
+        scan_keys<2, false>(kk, (okh ? 1u : 0u) | (okt ? 2u : 0u), slo, shi, clt, ceqlo, ceqhi, st);
     }
-    if constexpr (ORD) os.flush();  // the wave's last entries (and its candidates, reserved by the wave)
     // counts: wave reduce -> LDS -> one atomic per workgroup and counter; the
     // waves' final region fills are combined the same way, so the candidate
     // buffer sees one reservation per workgroup at the end of the pass
@@ -1155,8 +1177,8 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         red[0][wid] = r0;
         red[1][wid] = r1;
         red[2][wid] = r2;
-        red[3][wid] = ORD ? os.winside : st.winside;
-        red[4][wid] = ORD ? 0u : st.wfill;
+        red[3][wid] = (ORD ? os.winside : 0ull) + st.winside;
+        red[4][wid] = st.wfill;
     }
     __syncthreads();
     if (threadIdx.x < 5) {
@@ -1175,7 +1197,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         }
     }
     __syncthreads();
-    if (!ORD && st.wfill) {  // this wave's final region, at its share of the reservation
+    if (st.wfill) {  // this wave's final region, at its share of the reservation
         u64 g = red[5][0];
         for (int w = 0; w < wid; ++w) g += red[4][w];
         st.put(g, st.wfill);

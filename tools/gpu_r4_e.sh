@@ -35,11 +35,18 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 180 --timeout-method threa
 tail -1 $O/topk_tests.log
 echo "== tk5 A/B"
 for k in 1048576 16777216 67108864; do
-  for v in base tk5b4 tk5chunk; do
+  for v in base r3flush tk5b4 tk5chunk; do
     lib=mpi-k-selection_amd/lib/variants/libkth_$v.so; [ $v = base ] && lib=mpi-k-selection_amd/lib/libkth.so
     KTH_LIB=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/tk_${v}_$k -o run --output-format csv -- python3 bench.py --workload topk --k $k --steps 5 --warmup 2 --no-cpu-baseline > $O/tk_${v}_$k.log 2>&1 || { echo "$v rc=$?"; tail -20 $O/tk_${v}_$k.log; exit 1; }
     echo "k=$k $v: $(tail -1 $O/tk_${v}_$k.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms", d["verified"])')"
     python3 tools/prof_summary.py $(find $O/tk_${v}_$k -name "*kernel_trace.csv" | head -1) 0 | grep -E "tk5|k_main"
   done
+done
+echo "== k_main<5> flush cost (diagnostic variants, k = 2^26; wrong top-k by design)"
+for v in nostage nosegstore nocands; do
+  lib=mpi-k-selection_amd/lib/variants/libkth_$v.so
+  KTH_LIB=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/diag_$v -o run --output-format csv -- python3 bench.py --workload topk --k 67108864 --steps 5 --warmup 2 --no-cpu-baseline > $O/diag_$v.log 2>&1; rc=$?
+  [ $rc -le 1 ] || { echo "$v rc=$rc"; tail -20 $O/diag_$v.log; exit 1; }
+  echo "$v:"; python3 tools/prof_summary.py $(find $O/diag_$v -name "*kernel_trace.csv" | head -1) 0 | grep -E "k_main"
 done
 echo done
