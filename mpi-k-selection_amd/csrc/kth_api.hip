@@ -1043,7 +1043,8 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
     if (tf >= 5) {  // the staged entries (rows < ncov), then the ragged rows from the input
-        kth::k_tk5_count<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
+        auto tk5c = (u64)k * 64 >= (u64)n ? kth::k_tk5_count<true> : kth::k_tk5_count<false>;  // dense windows: chunked
+        tk5c<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
             c->tk_segv, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status, flip,
             c->tk_wcnt, tcnt);
         kth::k_topk_count<true, 2><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,

@@ -679,44 +679,86 @@ struct OrdStager {
     // 4-byte position stores (the segment is 16-byte aligned and a mid-pass
     // flush writes a multiple of 4 entries: the 0-3 left over move to the
     // region's front; `last` writes them too), and the flushed entries'
-    // candidates (lo < x < hi) to the candidate buffer.
+    // candidates (lo < x < hi) to the candidate buffer.  Latency, not work,
+    // is what a flush costs the streaming wave (it issues no loads meanwhile):
+    // every LDS read of a step is issued before any is used -- lane l takes
+    // the 4-entry groups l, l + 64, .. (FQ of them) -- and the candidates,
+    // an unordered multiset, are counted per lane, placed by one wave scan and
+    // one reservation, and written by each lane from its own groups (a
+    // ballot + mbcnt loop over the region waited one LDS round trip per 64
+    // entries, twice: ~2 us a flush, ~90 flushes a wave at k = n / 16).
+    static constexpr int FQ = (int)((CAP + 4 * WAVE - 1) / (4 * WAVE));  // 4-entry groups per lane
+    static constexpr int FH = (FQ + 1) / 2;                              // groups per half (registers)
     __device__ __forceinline__ void flush(bool last = false) {
         const int lane = threadIdx.x & (WAVE - 1);
         __builtin_amdgcn_wave_barrier();
         uint8_t *pb = reinterpret_cast<uint8_t *>(reg + CAP);
         const uint32_t n4 = wfill & ~3u, nw = last ? wfill : n4;  // entries written now
         const u64 base = seg_base + seg_fill;                     // a multiple of 4
-#ifndef KTH_DIAG_TK5_NOSEGSTORE  // diagnostic builds only (wrong top-k results): cost of the segment stores
         const uint32_t room = seg_fill < seg.cap ? seg.cap - seg_fill : 0u;  // entries the segment still holds
-        for (uint32_t q = lane; 4 * q < n4; q += WAVE)
-            if (4 * q + 4 <= room) {
-                *reinterpret_cast<uint4 *>(seg.vals + base + 4 * q) = reinterpret_cast<const uint4 *>(reg)[q];
-                *reinterpret_cast<uint32_t *>(seg.pos + base + 4 * q) = reinterpret_cast<const uint32_t *>(pb)[q];
+        const uint4 *r4 = reinterpret_cast<const uint4 *>(reg);
+        const uint32_t *p4 = reinterpret_cast<const uint32_t *>(pb);
+        auto is_cand = [&](uint32_t x, uint32_t e) { return e < nw && (int32_t)x > slo && (int32_t)x < shi; };
+        // pass 1: segment stores + this lane's candidate count, half the groups at a time
+        uint32_t nc = 0;
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+            uint4 kv[FH];
+            uint32_t pv[FH];
+#pragma unroll
+            for (int j = 0; j < FH; ++j) {
+                const uint32_t g = (uint32_t)((h * FH + j) * WAVE + lane);
+                kv[j] = 4 * g < nw ? r4[g] : make_uint4(0u, 0u, 0u, 0u);
+                pv[j] = 4 * g < nw ? p4[g] : 0u;
             }
-        if (last && (uint32_t)lane < wfill - n4 && n4 + lane < room) {  // the last 0-3 entries
-            seg.vals[base + n4 + lane] = (int32_t)reg[n4 + lane];
-            seg.pos[base + n4 + lane] = pb[n4 + lane];
-        }
+#pragma unroll
+            for (int j = 0; j < FH; ++j) {
+                const uint32_t g = (uint32_t)((h * FH + j) * WAVE + lane), e = 4 * g;
+#ifndef KTH_DIAG_TK5_NOSEGSTORE  // diagnostic builds only (wrong top-k results): cost of the segment stores
+                if (e + 4 <= n4 && e + 4 <= room) {
+                    *reinterpret_cast<uint4 *>(seg.vals + base + e) = kv[j];
+                    *reinterpret_cast<uint32_t *>(seg.pos + base + e) = pv[j];
+                } else if (last && e < nw) {  // the last 1-3 entries (unaligned tail)
+                    const uint32_t kq[4] = {kv[j].x, kv[j].y, kv[j].z, kv[j].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (e + q < nw && e + q < room) {
+                            seg.vals[base + e + q] = (int32_t)kq[q];
+                            seg.pos[base + e + q] = (uint8_t)(pv[j] >> (8 * q));
+                        }
+                }
 #endif
-        if (seg_fill + nw > seg.cap && lane == 0) *seg.ovf = 1u;
-        // the window's candidates -> the candidate buffer (one reservation)
-        uint32_t nin = 0;
-#ifndef KTH_DIAG_TK5_NOCANDS  // diagnostic builds only (wrong results): cost of the candidate filter
-        for (uint32_t i0 = 0; i0 < nw; i0 += WAVE) {
-            const int32_t x = (int32_t)reg[(i0 + lane) < nw ? i0 + lane : 0];
-            nin += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(i0 + lane < nw && x > slo && x < shi));
+                nc += (is_cand(kv[j].x, e) ? 1u : 0u) + (is_cand(kv[j].y, e + 1) ? 1u : 0u) +
+                      (is_cand(kv[j].z, e + 2) ? 1u : 0u) + (is_cand(kv[j].w, e + 3) ? 1u : 0u);
+            }
         }
-        if (nin) {
-            const u64 g = reserve_cands(cand_count, acc, cap, nin);
-            uint32_t o = 0;
-            for (uint32_t i0 = 0; i0 < nw; i0 += WAVE) {
-                const int32_t x = (int32_t)reg[(i0 + lane) < nw ? i0 + lane : 0];
-                const bool in = i0 + lane < nw && x > slo && x < shi;
-                const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
-                const uint32_t below =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
-                if (in && g + o + below < cap) put_cand(&cand_out[g + o + below], (uint32_t)x ^ 0x80000000u);
-                o += (uint32_t)__popcll(B);
+        if (seg_fill + nw > seg.cap && lane == 0) *seg.ovf = 1u;
+#ifndef KTH_DIAG_TK5_NOCANDS  // diagnostic builds only (wrong results): cost of the candidate filter
+        // pass 2: one reservation for the wave, each lane its candidates from its offset
+        const uint32_t incl = wave_incl_scan32(nc);
+        const uint32_t nin = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+        if (nin) {  // wave-uniform
+            const u64 g0 = reserve_cands(cand_count, acc, cap, nin);
+            u64 o = g0 + incl - nc;
+#pragma unroll 1
+            for (int h = 0; h < 2; ++h) {
+                uint4 kv[FH];
+#pragma unroll
+                for (int j = 0; j < FH; ++j) {
+                    const uint32_t g = (uint32_t)((h * FH + j) * WAVE + lane);
+                    kv[j] = 4 * g < nw ? r4[g] : make_uint4(0u, 0u, 0u, 0u);
+                }
+#pragma unroll
+                for (int j = 0; j < FH; ++j) {
+                    const uint32_t e = 4u * (uint32_t)((h * FH + j) * WAVE + lane);
+                    const uint32_t kq[4] = {kv[j].x, kv[j].y, kv[j].z, kv[j].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (is_cand(kq[q], e + q)) {
+                            if (o < cap) put_cand(&cand_out[o], kq[q] ^ 0x80000000u);
+                            ++o;
+                        }
+                }
             }
             winside += nin;
         }

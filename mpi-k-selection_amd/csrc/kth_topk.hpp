@@ -399,11 +399,11 @@ __device__ __forceinline__ uint32_t tk5_wstart(const uint32_t *wstart, uint32_t 
 // lane (a rolled per-entry loop waited one memory round trip per entry; 4 in
 // flight: one round trip per 4 entries); with sp, their positions are loaded
 // beside them (f(x, p)).
-#ifndef KTH_TK5_BATCH
-#define KTH_TK5_BATCH 16
+#ifndef KTH_TK5_BATCH  // (16: k_tk5_write 56 / 121 / 400 us at k = 2^20 / 2^24 / 2^26; 4: 38 / 115 / 411)
+#define KTH_TK5_BATCH 4
 #endif
-#ifndef KTH_TK5_CHUNKED  // 1: the window's entries staged in LDS by coalesced chunks (A/B)
-#define KTH_TK5_CHUNKED 0
+#ifndef KTH_TK5_CHUNKED  // 1: k_tk5_write stages the window's entries in LDS by coalesced chunks (A/B:
+#define KTH_TK5_CHUNKED 0  // 82 / 165 / 619 us -- the LDS costs the write kernel occupancy)
 #endif
 template <typename F>
 __device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
@@ -454,52 +454,53 @@ __device__ __forceinline__ void tk5_chunk_load(const T *__restrict__ sv, uint32_
 
 // Per wave-row: #better | #equal << 16 -> wcnt; per row (the 4 wave-rows of
 // its 4 waves, summed through LDS) -> tcnt.  Entries are read, the input is not.
+// CHUNKED (dense windows, k >= n / 64): the window's entries come in by
+// coalesced chunks (tk5_chunk_load); sparse windows walk each wave-row's few
+// entries per lane (k = 2^20 / 2^24 / 2^26: lane walk 21.7 / 37.1 / 169 us,
+// chunked 30.0 / 33.8 / 95 us).
+template <bool CHUNKED>
 __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restrict__ segv, u64 seg_cap,
                                                         const uint32_t *__restrict__ wstart, uint32_t nwin, u64 G,
                                                         const uint32_t *__restrict__ tflags, u64 nfull,
                                                         const int32_t *__restrict__ d_v, uint32_t flip,
                                                         uint32_t *__restrict__ wcnt, uint32_t *__restrict__ tcnt) {
     __shared__ uint32_t part[TK_BLOCK / WAVE][WAVE];
-#if KTH_TK5_CHUNKED
-    __shared__ uint32_t ecode[TK_BLOCK / WAVE][TK5_ECHUNK];  // an entry's #better | #equal << 16
-#endif
+    __shared__ uint32_t ecode[TK_BLOCK / WAVE][CHUNKED ? TK5_ECHUNK : 1];  // an entry's #better | #equal << 16
     if (!tk5_ok(tflags, d_v)) return;  // grid-uniform
     const int32_t v = d_v[0];
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const Tk5Part P = tk5_part(nfull, G);
     const int32_t *sv = segv + (P.b * (TK_BLOCK / WAVE) + w) * seg_cap;
     const uint32_t *ws = tflags + TF_W0 + (P.b * (TK_BLOCK / WAVE) + w) * rw_seg_words(nfull, G);  // this wave's row words
-#if KTH_TK5_CHUNKED
     uint32_t *ec = ecode[w];
-#endif
     for (u64 win = P.w_lo; win < P.w_hi; ++win) {  // same trip count in the 4 waves
         const u64 j = win * WAVE + lane;
         const bool valid = j < P.m;
         const u64 r = (P.b + (j / MAIN_UNROLL) * P.G) * MAIN_UNROLL + j % MAIN_UNROLL;
         const uint32_t c = valid ? ws[j] : 0u;
         const uint32_t incl = wave_incl_scan32(c), s0 = incl - c;
-#if !KTH_TK5_CHUNKED
-        uint32_t nb = 0, ne = 0;
-        tk5_entries(sv + tk5_wstart(wstart, nwin, P.b, w, win) + s0, nullptr, c, [&](int32_t x, uint8_t) {
-            nb += (flip == 0u ? x < v : x > v) ? 1u : 0u;
-            ne += x == v ? 1u : 0u;
-        });
-        const uint32_t word = nb | ne << 16;
-#else
-        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);  // the window's entries
-        const uint32_t ws0 = tk5_wstart(wstart, nwin, P.b, w, win);
         uint32_t word = 0;
-        for (uint32_t c0 = 0; c0 < T; c0 += TK5_ECHUNK) {  // wave-uniform
-            const uint32_t cn = T - c0 < (uint32_t)TK5_ECHUNK ? T - c0 : (uint32_t)TK5_ECHUNK;
-            tk5_chunk_load(sv, ws0, c0, cn, [&](uint32_t e, int32_t x) {
-                ec[e] = ((flip == 0u ? x < v : x > v) ? 1u : 0u) | (x == v ? 0x10000u : 0u);
+        if constexpr (!CHUNKED) {
+            uint32_t nb = 0, ne = 0;
+            tk5_entries(sv + tk5_wstart(wstart, nwin, P.b, w, win) + s0, nullptr, c, [&](int32_t x, uint8_t) {
+                nb += (flip == 0u ? x < v : x > v) ? 1u : 0u;
+                ne += x == v ? 1u : 0u;
             });
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t lo = tk5_clip(s0, c0, cn), hi = tk5_clip(incl, c0, cn);
-            for (uint32_t e = lo; e < hi; ++e) word += ec[e];
-            __builtin_amdgcn_wave_barrier();  // the chunk's LDS is rewritten next
+            word = nb | ne << 16;
+        } else {
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);  // the window's entries
+            const uint32_t ws0 = tk5_wstart(wstart, nwin, P.b, w, win);
+            for (uint32_t c0 = 0; c0 < T; c0 += TK5_ECHUNK) {  // wave-uniform
+                const uint32_t cn = T - c0 < (uint32_t)TK5_ECHUNK ? T - c0 : (uint32_t)TK5_ECHUNK;
+                tk5_chunk_load(sv, ws0, c0, cn, [&](uint32_t e, int32_t x) {
+                    ec[e] = ((flip == 0u ? x < v : x > v) ? 1u : 0u) | (x == v ? 0x10000u : 0u);
+                });
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t lo = tk5_clip(s0, c0, cn), hi = tk5_clip(incl, c0, cn);
+                for (uint32_t e = lo; e < hi; ++e) word += ec[e];
+                __builtin_amdgcn_wave_barrier();  // the chunk's LDS is rewritten next
+            }
         }
-#endif
         if (valid) wcnt[r * (TK_BLOCK / WAVE) + w] = word;
         part[w][lane] = word;
         __syncthreads();

@@ -1,0 +1,18 @@
+# Round 4 evidence (a): the whole GPU suite, smoke(), the default bench line
+# (the driver's N=1 command, with CPU baselines) and its rocprof kernel stats.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/fa; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
+echo "== pytest -m gpu"
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 180 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo tests rc=$?; grep -E "FAIL|Error" $O/gpu_tests.log | head -20; tail -5 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+echo "== smoke"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke rc=$?; tail -20 $O/smoke.log; exit 1; }
+tail -3 $O/smoke.log
+echo "== bench (driver command)"
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1 || { echo bench rc=$?; tail -20 $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-700
+echo "== rocprof (driver command, no CPU baselines)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1 || { echo prof rc=$?; tail -20 $O/prof.log; exit 1; }
+python3 tools/prof_summary.py $O/prof/run_kernel_trace.csv > $O/select_summary.txt; head -8 $O/select_summary.txt
+python3 tools/prof_calls.py $O/prof/run_kernel_trace.csv > $O/select_calls.txt; tail -3 $O/select_calls.txt | cut -c1-300
+echo done

@@ -1,0 +1,37 @@
+# Round 4 evidence (b): PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE
+# passes) on the final build for the select, the rows and the staged top-k;
+# the 2^33 lines; the warmup transient with and without candidate staging.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/fb; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
+pmc2() {  # pmc2 NAME -- bench args: two passes, csv paths in $O/pmc_NAME_{FETCH,WRITE}_SIZE
+  local name=$1; shift 2
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 180 rocprofv3 --pmc $c -d $O/pmc_${name}_$c -o run --output-format csv -- python3 bench.py "$@" > $O/pmc_${name}_$c.log 2>&1 || { echo pmc $name $c rc=$?; tail -20 $O/pmc_${name}_$c.log; exit 1; }
+  done
+}
+csv() { find $O/pmc_$1_$2 -name "*counter_collection.csv" | head -1; }
+echo "== PMC select"
+pmc2 select -- --steps 3 --warmup 1 --no-cpu-baseline
+python3 tools/pmc_traffic.py $(csv select FETCH_SIZE) $(csv select WRITE_SIZE) k_main 30 uniform_half $O/pmc_traffic.json | tail -4
+for dt in i32 f32; do
+  echo "== PMC rows $dt"
+  pmc2 rows_$dt -- --workload rows --rows-dtype $dt --k 64 --steps 3 --warmup 1
+  python3 tools/pmc_traffic.py $(csv rows_$dt FETCH_SIZE) $(csv rows_$dt WRITE_SIZE) rows_reg 28 rows_$dt $O/pmc_traffic_rows_$dt.json | tail -4
+done
+for k in 1048576 67108864; do
+  echo "== PMC top-k k=$k"
+  pmc2 topk_$k -- --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline
+  python3 tools/pmc_topk.py $(csv topk_$k FETCH_SIZE) $(csv topk_$k WRITE_SIZE) 30 uniform_half $k $O/pmc_traffic_topk_k$k.json
+done
+echo "== 2^33 lines"
+timeout -k 10 300 python -u bench.py --log2n 33 --steps 10 --warmup 3 --no-cpu-baseline > $O/b33.log 2>&1 || { echo b33 rc=$?; tail -20 $O/b33.log; exit 1; }
+tail -1 $O/b33.log | cut -c1-300
+timeout -k 10 300 python -u bench.py --log2n 30 --local-shards 8 --steps 10 --warmup 3 --no-cpu-baseline > $O/b8.log 2>&1 || { echo b8 rc=$?; tail -20 $O/b8.log; exit 1; }
+tail -1 $O/b8.log | cut -c1-300
+echo "== warmup transient: k_main per call, base vs no candidate staging (diagnostic build)"
+for v in base nostage0; do
+  lib=mpi-k-selection_amd/lib/variants/libkth_$v.so; [ $v = base ] && lib=mpi-k-selection_amd/lib/libkth.so
+  KTH_LIB=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace -d $O/bump_$v -o run --output-format csv -- python3 tools/bump_probe.py uniform_half > $O/bump_$v.log 2>&1 || { echo "bump $v rc=$?"; tail -20 $O/bump_$v.log; exit 1; }
+  echo "$v:"; python3 tools/prof_calls.py $(find $O/bump_$v -name "*kernel_trace.csv" | head -1) | grep "k_main" | cut -c1-420
+done
+echo done
