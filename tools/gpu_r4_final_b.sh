@@ -28,6 +28,14 @@ timeout -k 10 300 python -u bench.py --log2n 33 --steps 10 --warmup 3 --no-cpu-b
 tail -1 $O/b33.log | cut -c1-300
 timeout -k 10 300 python -u bench.py --log2n 30 --local-shards 8 --steps 10 --warmup 3 --no-cpu-baseline > $O/b8.log 2>&1 || { echo b8 rc=$?; tail -20 $O/b8.log; exit 1; }
 tail -1 $O/b8.log | cut -c1-300
+echo "== SQ mix per 64-key slot: select k_main<0> vs staged top-k k_main<5> (k = 2^20, 2^26)"
+C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES"
+timeout -s KILL 120 rocprofv3 --pmc $C -d $O/sq_sel -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_sel.log 2>&1 || { echo sq rc=$?; tail -20 $O/sq_sel.log; exit 1; }
+python3 tools/sq_mix.py $O/sq_sel "k_main<0>" 1073741824 "select k_main<0>"
+for k in 1048576 67108864; do
+  timeout -s KILL 120 rocprofv3 --pmc $C -d $O/sq_tk_$k -o run --output-format csv -- python3 bench.py --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_tk_$k.log 2>&1 || { echo sq rc=$?; tail -20 $O/sq_tk_$k.log; exit 1; }
+  python3 tools/sq_mix.py $O/sq_tk_$k "k_main<5>" 1073741824 "top-k k=$k k_main<5>"
+done
 echo "== warmup transient: k_main per call, base vs no candidate staging (diagnostic build)"
 for v in base nostage0; do
   lib=mpi-k-selection_amd/lib/variants/libkth_$v.so; [ $v = base ] && lib=mpi-k-selection_amd/lib/libkth.so
