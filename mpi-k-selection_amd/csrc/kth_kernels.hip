@@ -619,6 +619,21 @@ struct Stager {
         wfill = 0;
     }
 
+    // One key slot of the wave, as the streaming pass sees it: `near` = this
+    // lane's key lies in the closed window [lo, hi].  Only a slot where some
+    // lane's key does (uniform keys: ~1/3 of the slots at 2^30) tells the
+    // edges from the inside: the keys equal to lo / hi are counted, the
+    // others are staged.  (Counting both edges on every key cost two compares
+    // and two adds per key; with them here the pass issues ~3 VALU ops a key
+    // fewer.)
+    __device__ __forceinline__ void slot_near(int32_t x, bool near, int32_t slo, int32_t shi, uint32_t &ceqlo,
+                                              uint32_t &ceqhi, uint32_t row = ~0u) {
+        if (__builtin_amdgcn_ballot_w64(near) == 0) return;  // wave-uniform
+        ceqlo += (near & (x == slo)) ? 1u : 0u;
+        ceqhi += (near & (x == shi)) ? 1u : 0u;
+        slot((uint32_t)x ^ 0x80000000u, near & (x != slo) & (x != shi), row);
+    }
+
     // One key slot of the wave: `in` = this lane's key is a candidate.
     __device__ __forceinline__ void slot(uint32_t key, bool in, uint32_t row = ~0u) {
         const unsigned long long B = __builtin_amdgcn_ballot_w64(in);
@@ -788,8 +803,11 @@ struct OrdStager {
     // of its 4 keys (the usual case: ~1-2 % of the keys are staged), a key's
     // slot is the fill plus mbcnt of the OR'ed ballots and the key is picked by
     // selects on the ballots; otherwise a wave scan of the per-lane counts.
+    // The keys equal to lo / hi are on the kept side too, so they are counted
+    // here, behind the same wave-uniform test (ceqlo / ceqhi: this lane's).
     template <int TF>
-    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t valid4, uint32_t p0) {
+    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t valid4, uint32_t p0, uint32_t &ceqlo,
+                                            uint32_t &ceqhi) {
         auto f1 = [&](uint32_t x, int j) {
             return ((valid4 >> j) & 1u) != 0u && (TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo);
         };
@@ -798,6 +816,13 @@ struct OrdStager {
                                  b2 = __builtin_amdgcn_ballot_w64(c2), b3 = __builtin_amdgcn_ballot_w64(c3);
         const unsigned long long any = b0 | b1 | b2 | b3;
         if (any == 0) return 0u;  // wave-uniform
+        {
+            const int32_t x0 = (int32_t)q.x, x1 = (int32_t)q.y, x2 = (int32_t)q.z, x3 = (int32_t)q.w;
+            ceqlo += ((c0 & (x0 == slo)) ? 1u : 0u) + ((c1 & (x1 == slo)) ? 1u : 0u) +
+                     ((c2 & (x2 == slo)) ? 1u : 0u) + ((c3 & (x3 == slo)) ? 1u : 0u);
+            ceqhi += ((c0 & (x0 == shi)) ? 1u : 0u) + ((c1 & (x1 == shi)) ? 1u : 0u) +
+                     ((c2 & (x2 == shi)) ? 1u : 0u) + ((c3 & (x3 == shi)) ? 1u : 0u);
+        }
         const uint32_t total = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
 #ifdef KTH_DIAG_TK5_NOSTAGE  // diagnostic builds only (wrong top-k results): cost of the staging
         return total;
@@ -861,19 +886,20 @@ __device__ __forceinline__ void scan_keys(const uint32_t (&xw)[K], uint32_t vali
                                           uint32_t &clt, uint32_t &ceqlo, uint32_t &ceqhi, Stager<ROWS> &st,
                                           uint32_t row0 = ~0u, RowAcc *ra = nullptr) {
     static_assert(RW == 0 || (FULL && K == 32), "row tallies cover a full tile's 8 rows");
+    const uint32_t span = (uint32_t)shi - (uint32_t)slo;  // [lo, hi] as an unsigned distance from lo (key order)
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const int32_t x = (int32_t)xw[j];
         const bool ok = FULL || ((valid >> j) & 1u);
         clt += (ok & (x < slo)) ? 1u : 0u;
-        ceqlo += (ok & (x == slo)) ? 1u : 0u;
-        ceqhi += (ok & (x == shi)) ? 1u : 0u;
         if constexpr (RW == 3) {  // #<lo is clt's own count: a snapshot after each row's 4 keys
             if ((j & 3) == 3) ra->r[j / 4] = clt;
         } else if constexpr (RW == 4) {
             ra->r[j / 4] += x > shi ? 1u : 0u;
         }
-        st.slot((uint32_t)x ^ 0x80000000u, ok & (x > slo) & (x < shi), row0 == ~0u ? ~0u : row0 + (uint32_t)(j / 4));
+        // (x - lo as u32 is the distance in key order: flipping the sign bit is adding 2^31)
+        st.slot_near(x, ok & (xw[j] - (uint32_t)slo <= span), slo, shi, ceqlo, ceqhi,
+                     row0 == ~0u ? ~0u : row0 + (uint32_t)(j / 4));
     }
 }
 
@@ -1006,10 +1032,8 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             const int32_t x = (int32_t)k4[j];
             const bool ok = (valid4 >> j) & 1u;
             clt += (ok & (x < slo)) ? 1u : 0u;
-            ceqlo += (ok & (x == slo)) ? 1u : 0u;
-            ceqhi += (ok & (x == shi)) ? 1u : 0u;
         }
-        return os.template row<TF>(q, valid4, p0);
+        return os.template row<TF>(q, valid4, p0, ceqlo, ceqhi);  // (the edges are counted there)
     };
 
     // a tile is consumed in groups of 4 * MAIN_SUB keys
