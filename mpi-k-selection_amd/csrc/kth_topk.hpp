@@ -402,9 +402,12 @@ __device__ __forceinline__ uint32_t tk5_wstart(const uint32_t *wstart, uint32_t 
 #ifndef KTH_TK5_BATCH  // (16: k_tk5_write 56 / 121 / 400 us at k = 2^20 / 2^24 / 2^26; 4: 38 / 115 / 411)
 #define KTH_TK5_BATCH 4
 #endif
-#ifndef KTH_TK5_CHUNKED  // 1: k_tk5_write stages the window's entries in LDS by coalesced chunks (A/B:
-#define KTH_TK5_CHUNKED 0  // 82 / 165 / 619 us -- the LDS costs the write kernel occupancy)
-#endif
+// (Two other k_tk5_write placements were measured and removed: staging each
+// window's entries in LDS by coalesced chunks, 82 / 165 / 619 us at k = 2^20 /
+// 2^24 / 2^26 (the LDS cost occupancy); and taking the window's entries 64 at a
+// time, one per lane, with each entry's wave-row found by a DPP max-scan over
+// LDS-marked wave-row starts and its position from ballot prefix counts,
+// 40 / 110 / 499 us against this walk's 38 / 112 / 427 on one box.)
 template <typename F>
 __device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
                                             uint32_t c, F &&f) {
@@ -559,10 +562,6 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
     __shared__ uint16_t s_loc[TK5_STAGE];  // key index within its tile: u << 10 | w << 8 | position
     __shared__ u64 s_lo[8];                // tile i of the window: its first output slot
     __shared__ uint32_t s_off[9];          // and its first stage entry (s_off[8]: the window's total)
-#if KTH_TK5_CHUNKED
-    __shared__ int32_t e_val[TK_BLOCK / WAVE][TK5_ECHUNK];  // a chunk of each wave's window entries
-    __shared__ uint8_t e_pos[TK_BLOCK / WAVE][TK5_ECHUNK];
-#endif
     if (!tk5_ok(tflags, d_v) || meta[1]) return;  // grid-uniform
     const u64 need = meta[0];
     const int32_t v = d_v[0];
@@ -636,23 +635,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_write(const int32_t *__restric
                 }
             }
         };
-#if !KTH_TK5_CHUNKED
         tk5_entries(segv + sbase + start, segp + sbase + start, c, place);
-#else
-        const uint32_t incl = start - wbase + c, s0 = incl - c;  // this lane's entries in the window: [s0, incl)
-        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
-        int32_t *evw = e_val[w];
-        uint8_t *epw = e_pos[w];
-        for (uint32_t c0 = 0; c0 < T; c0 += TK5_ECHUNK) {  // wave-uniform
-            const uint32_t cn = T - c0 < (uint32_t)TK5_ECHUNK ? T - c0 : (uint32_t)TK5_ECHUNK;
-            tk5_chunk_load(segv + sbase, wbase, c0, cn, [&](uint32_t e, int32_t x) { evw[e] = x; });
-            tk5_chunk_load(segp + sbase, wbase, c0, cn, [&](uint32_t e, uint8_t x) { epw[e] = x; });
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t lo = tk5_clip(s0, c0, cn), hi = tk5_clip(incl, c0, cn);
-            for (uint32_t e = lo; e < hi; ++e) place(evw[e], epw[e]);
-            __builtin_amdgcn_wave_barrier();  // the chunk's LDS is rewritten next
-        }
-#endif
         if (staged) {  // coalesced copy-out, tile by tile
             __syncthreads();
             const u64 tile0 = (b + (j0 / MAIN_UNROLL) * G) * MAIN_UNROLL * TK_TILE;  // the window's first tile's first key

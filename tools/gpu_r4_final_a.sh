@@ -15,4 +15,24 @@ echo "== rocprof (driver command, no CPU baselines)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof.log 2>&1 || { echo prof rc=$?; tail -20 $O/prof.log; exit 1; }
 python3 tools/prof_summary.py $O/prof/run_kernel_trace.csv > $O/select_summary.txt; head -8 $O/select_summary.txt
 python3 tools/prof_calls.py $O/prof/run_kernel_trace.csv > $O/select_calls.txt; tail -3 $O/select_calls.txt | cut -c1-300
+echo "== top-k sweep"
+for k in 1024 1048576 16777216 67108864 134217728 536870912; do
+  timeout -k 10 120 python -u bench.py --workload topk --k $k --steps 10 --warmup 3 --no-cpu-baseline >> $O/topk.jsonl 2>$O/topk.err || { echo topk rc=$?; tail -20 $O/topk.err; exit 1; }
+done
+python3 -c "
+import json
+for l in open('$O/topk.jsonl'):
+    d=json.loads(l); print('topk k', d['config']['k'], round(d['ms_per_step'],3), 'ms', round(d['value'],1), 'Gkeys/s', d.get('verified'))"
+echo "== config 4 (adversarial families at 2^30)"
+N=$((1 << 30))
+for fam in uniform_half all_equal few_distinct sorted_asc sorted_desc; do
+  for k in 1 $((N / 2)) $N; do
+    timeout -k 10 120 python -u bench.py --family $fam --k $k --steps 20 --warmup 5 --no-cpu-baseline >> $O/adv.jsonl 2>$O/adv.err || { echo "$fam k=$k rc=$?"; tail -20 $O/adv.err; exit 1; }
+  done
+done
+python3 -c "
+import json
+for l in open('$O/adv.jsonl'):
+    d=json.loads(l); c=d['config']
+    print(c.get('family', '?'), 'k', c.get('k'), round(d['value'],1), 'Gkeys/s', round(d['ms_per_step'],4), 'ms', 'path', d.get('path'), 'cands', d.get('candidates'), d['verified'])"
 echo done
