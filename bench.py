@@ -334,10 +334,14 @@ def rows_main(args):
         verified = bool(torch.equal(out[:chk], want))
     keys_total = R * C * world
     value = keys_total / (elapsed / args.steps) / 1e9
-    achieved = 4.0 * R * C / (kern_ms * 1e-3) / 1e9
+    # algorithmic bytes of a launch: the keys read, the outputs written (top-k:
+    # a value and an int32 column per kept key; k-th: one value per row)
+    algo_bytes = 4 * R * C + (8 * R * k if args.topk else 4 * R)
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
     rows_traffic, rows_note = None, "no PMC measurement for this workload"
-    if not args.topk and not dup and (R, C, k) == (65536, 4096, 64):
-        rows_traffic, rows_note = pmc_traffic(f"pmc_traffic_rows_{args.rows_dtype}.json", None, None)
+    if not dup and (R, C, k) == (65536, 4096, 64):
+        rows_traffic, rows_note = pmc_traffic(
+            f"pmc_traffic_rows_{'topk_' if args.topk else ''}{args.rows_dtype}.json", None, None)
     res = {
         "metric": ("Gkeys/s batched top-k (largest) per row" if args.topk else "Gkeys/s batched k-th per row")
                   + " (65536 x 4096, BASELINE config 5)",
@@ -353,7 +357,7 @@ def rows_main(args):
         "roofline": {"bound": "hbm", "kernel": "kth::k_rows_reg" if C <= 4096 else "kth::k_rows",
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": rows_traffic, "traffic_source": rows_note,
-                     "algorithmic_bytes_per_launch": 4 * R * C, "avg_launch_ms": kern_ms},
+                     "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": kern_ms},
         "verified": verified,
     }
     if rank == 0:

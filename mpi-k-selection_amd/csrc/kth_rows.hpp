@@ -31,6 +31,9 @@ constexpr bool TOPK_RELOAD = KTH_TOPK_RELOAD;  // top-k compaction re-reads full
 #ifndef KTH_ROWS_WAVES
 #define KTH_ROWS_WAVES 4  // waves per SIMD the register budget is held to (<= 128 VGPRs)
 #endif
+#ifndef KTH_TOPK_ROWS_WAVES
+#define KTH_TOPK_ROWS_WAVES KTH_ROWS_WAVES  // the same for the top-k rows kernels
+#endif
 constexpr int RW_BINS = 256;
 constexpr int RW_STRIDE = RW_BINS + 4;  // words between histogram copies: 16-B aligned, a bin's copies in different banks
 
@@ -637,10 +640,16 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
                 __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
             }
         };
+#ifndef KTH_DIAG_ROWS_NOSTAGE  // (timing diagnostics only: wrong results)
         if (F32 && vmap)
             stage_rows(std::true_type{});
         else
             stage_rows(std::false_type{});
+#endif
+#ifdef KTH_DIAG_ROWS_NOTAIL
+        *topk_done = true;
+        return staged;
+#endif
         __builtin_amdgcn_wave_barrier();
         // the list: the staged keys of bin B (a handful of rounds over <= nc pairs)
         for (uint32_t i0 = 0; i0 < staged; i0 += WAVE) {  // wave-uniform
@@ -694,7 +703,9 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     __builtin_amdgcn_wave_barrier();
     if (STAGE && stage) {
         // the staged pairs in column order: keep the keys below the k-th and the
-        // first kk keys equal to it (ties by column)
+        // first kk keys equal to it (ties by column).  (Staging the kept pairs in
+        // LDS for one pass of 16-byte stores measured the same: the output's
+        // cost is its DRAM writes, not the store instructions.)
         const uint32_t *skey = hist + STAGE_OFF, *scol = skey + stage_cap<R0>();
         const uint32_t nc = below + cnt;
         uint32_t out = 0, eq_seen = 0;
@@ -709,10 +720,14 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
             const bool keep = lt2 || (eq2 && rank < kk);
             const unsigned long long bk = __ballot(keep);
             const uint32_t pos = out + __builtin_amdgcn_mbcnt_hi((uint32_t)(bk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bk, 0u));
+#ifndef KTH_DIAG_ROWS_NOSTORE  // (timing diagnostics only: no output)
             if (keep) {
                 if (tko->vals) tko->vals[tko->obase + pos] = (F32 && vmap) ? pr.x : raw_of_key<F32>(pr.x ^ flip);
                 if (tko->idx) tko->idx[tko->obase + pos] = (int32_t)pr.y;
             }
+#else
+            asm volatile("" ::"v"(pos), "v"(pr.x), "v"(pr.y), "v"((uint32_t)keep));
+#endif
             out += (uint32_t)__popcll(bk);
             eq_seen += (uint32_t)__popcll(be);
         }
@@ -731,7 +746,7 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
 // order reversed: ~key).
 // FULL: cols == 64 * KPL and 16-byte aligned rows (unguarded loads, row_select_fast).
 template <bool F32, int KPL, bool VEC, int R0, bool TOPK, bool FULL>
-__global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL)) ? 2 : KTH_ROWS_WAVES) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
+__global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL)) ? 2 : TOPK ? KTH_TOPK_ROWS_WAVES : KTH_ROWS_WAVES) void k_rows_reg(const uint32_t *__restrict__ m, u64 rows, uint32_t cols,
                                                       uint32_t k, uint32_t *__restrict__ out, uint32_t flip,
                                                       uint32_t *__restrict__ vals, int32_t *__restrict__ idx) {
     static_assert(KPL % 4 == 0, "16-byte loads");
@@ -775,7 +790,11 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
             }
             answer = row_select_radix<KPL, R0>(key, hist, lane, kk);
 #else
+#ifndef KTH_DIAG_ROWS_SMALLOUT
             const TopkOut tko{k, vals, idx, r * (u64)k};
+#else  // (timing only: every row's output to one of 64 row slots, L2-resident)
+            const TopkOut tko{k, vals, idx, (r & 63) * (u64)k};
+#endif
             answer = row_select_fast<F32, KPL, R0, TOPK, TOPK>(key, hist, lane, kk, TOPK ? flip : 0u,
                                                                 TOPK ? &eqn : nullptr, &tko, &topk_done);
 #endif
@@ -804,7 +823,11 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
 #endif
         }
         if (!TOPK) {
+#ifndef KTH_DIAG_ROWS_NOOUT
             if (lane == 0) out[r] = raw_of_key<F32>(answer ^ flip);
+#else
+            asm volatile("" ::"v"(answer));
+#endif
         } else if (!topk_done) {
             // Compaction in column order.  Group j holds columns (64*j + lane)*4 + q:
             // lane-major, then q.  For each q a ballot of the selected keys and

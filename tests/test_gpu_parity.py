@@ -625,3 +625,36 @@ def test_rows_full_shape(gpu, f32):
         gpu.rows(m, R, C, k, out, f32=f32)
         gpu.sync()
         assert torch.equal(out, srt[:, k - 1]), k
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_topk_rows_many_rows(gpu, f32):
+    """Top-k rows over more rows than the resident waves (several rounds of the
+    row loop, the next row's loads in flight during the tail), with staged,
+    unstaged (ties) and dense-bin rows interleaved, against a stable sort."""
+    import torch
+    R, C, k = 16384 + 5, 4096, 64
+    g = torch.Generator(device="cuda")
+    g.manual_seed(321 + f32)
+    if f32:
+        m = torch.rand((R, C), generator=g, device="cuda") * 2 - 1
+        m[::7] = torch.round(m[::7] * 8) / 8
+        m[3::11] = torch.round(m[3::11] * 2000) / 2000
+        u = m.view(torch.int32).to(torch.int64)
+        key = torch.where(u < 0, -(u & 0x7FFFFFFF) - 1, u)  # the float order (no NaN here)
+    else:
+        m = torch.randint(-2 ** 31, 2 ** 31, (R, C), generator=g, device="cuda", dtype=torch.int64).to(torch.int32)
+        m[::7] = torch.randint(-3, 3, (len(range(0, R, 7)), C), generator=g, device="cuda", dtype=torch.int32)
+        m[3::11] = torch.randint(0, 1000, (len(range(3, R, 11)), C), generator=g, device="cuda", dtype=torch.int32)
+        key = m.to(torch.int64)
+    torch.cuda.synchronize()
+    for largest in (False, True):
+        order = -key if largest else key
+        want = torch.sort(torch.sort(order, dim=1, stable=True).indices[:, :k], dim=1).values.to(torch.int32)
+        vals = torch.empty((R, k), dtype=m.dtype, device="cuda")
+        idx = torch.empty((R, k), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        gpu.topk_rows(m, R, C, k, vals, idx, largest=largest, f32=f32)
+        gpu.sync()
+        assert torch.equal(idx, want), largest
+        assert torch.equal(vals.view(torch.int32), torch.gather(m, 1, want.to(torch.int64)).view(torch.int32)), largest

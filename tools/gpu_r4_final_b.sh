@@ -18,6 +18,11 @@ for dt in i32 f32; do
   pmc2 rows_$dt -- --workload rows --rows-dtype $dt --k 64 --steps 3 --warmup 1
   python3 tools/pmc_traffic.py $(csv rows_$dt FETCH_SIZE) $(csv rows_$dt WRITE_SIZE) rows_reg 28 rows_$dt $O/pmc_traffic_rows_$dt.json | tail -4
 done
+for dt in i32 f32; do
+  echo "== PMC top-k rows $dt"
+  pmc2 rows_topk_$dt -- --workload rows --rows-dtype $dt --topk --k 64 --steps 3 --warmup 1
+  python3 tools/pmc_traffic.py $(csv rows_topk_$dt FETCH_SIZE) $(csv rows_topk_$dt WRITE_SIZE) rows_reg 28 rows_topk_$dt $O/pmc_traffic_rows_topk_$dt.json 33554432 | tail -4
+done
 for k in 1048576 67108864; do
   echo "== PMC top-k k=$k"
   pmc2 topk_$k -- --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline

@@ -1,0 +1,18 @@
+# Round 4 (n): staged top-k rows with 16-byte output stores: rows parity, then
+# the config-5 top-k workloads against the 4-byte-store build (novout)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r4n; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
+: 
+: 
+: 
+L=mpi-k-selection_amd/lib
+one() {  # lib args
+  KTH_LIB=$1 timeout -k 10 120 python -u bench.py --workload rows $2 --k 64 --steps 20 --warmup 3 --no-cpu-baseline > $O/rows.log 2>&1; rc=$?
+  [ $rc -le 1 ] || { echo "bench rc=$rc"; tail -20 $O/rows.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('$O/rows.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$(basename $1)', '$2', round(d['value'],1), 'Gkeys/s kernel', round(r['avg_launch_ms']*1e3,1), 'us', d['verified'])"
+}
+for rep in 1 2; do
+  for lib in $L/libkth.so $L/variants/libkth_novout.so $L/variants/libkth_dsmallout.so $L/variants/libkth_dsmallout_nov.so; do one $lib "--rows-dtype i32 --topk" || exit 1; one $lib "--rows-dtype f32 --topk" || exit 1; done
+done
+one $L/libkth.so "--rows-dtype i32" && one $L/libkth.so "--rows-dtype f32"
+echo done

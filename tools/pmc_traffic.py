@@ -1,6 +1,9 @@
 """HBM traffic of the dominant kernel from two rocprofv3 --pmc passes.
 
-Usage: pmc_traffic.py FETCH_csv WRITE_csv KERNEL_SUBSTR LOG2N FAMILY OUT_JSON
+Usage: pmc_traffic.py FETCH_csv WRITE_csv KERNEL_SUBSTR LOG2N FAMILY OUT_JSON [OUT_BYTES]
+
+The algorithmic bytes are the 4-byte keys (2^LOG2N of them) read plus
+OUT_BYTES written (default 0; e.g. 8 * rows * k for top-k rows).
 
 Per MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B per
@@ -29,11 +32,12 @@ def per_dispatch(path, kernel, counter):
 
 
 fetch_csv, write_csv, kernel, log2n, family, out = sys.argv[1:7]
+out_bytes = float(sys.argv[7]) if len(sys.argv) > 7 else 0.0
 fetch_kib, nf = per_dispatch(fetch_csv, kernel, "FETCH_SIZE")
 write_kib, nw = per_dispatch(write_csv, kernel, "WRITE_SIZE")
 read_bytes = 2.0 * fetch_kib * 1024  # gfx950 FETCH_SIZE = 1/2 of 16-B-per-lane streaming reads
 write_bytes = write_kib * 1024
-algo = 4.0 * (1 << int(log2n))
+algo = 4.0 * (1 << int(log2n)) + out_bytes
 res = {
     "kernel": kernel,
     "log2n": int(log2n),
