@@ -402,12 +402,15 @@ __device__ __forceinline__ uint32_t tk5_wstart(const uint32_t *wstart, uint32_t 
 #ifndef KTH_TK5_BATCH  // (16: k_tk5_write 56 / 121 / 400 us at k = 2^20 / 2^24 / 2^26; 4: 38 / 115 / 411)
 #define KTH_TK5_BATCH 4
 #endif
-// (Two other k_tk5_write placements were measured and removed: staging each
-// window's entries in LDS by coalesced chunks, 82 / 165 / 619 us at k = 2^20 /
-// 2^24 / 2^26 (the LDS cost occupancy); and taking the window's entries 64 at a
-// time, one per lane, with each entry's wave-row found by a DPP max-scan over
-// LDS-marked wave-row starts and its position from ballot prefix counts,
-// 40 / 110 / 499 us against this walk's 38 / 112 / 427 on one box.)
+// (Three other k_tk5_write placements were measured and removed: staging each
+// window's entries in LDS by coalesced chunks of 1024, 82 / 165 / 619 us at
+// k = 2^20 / 2^24 / 2^26, and of 256 (1.25 KiB a wave), 137 / 252 / 982 us at
+// k = 2^24 / 2^25 / 2^26 against this walk's 118 / 205 / 421; and taking the
+// window's entries 64 at a time, one per lane, with each entry's wave-row
+// found by a DPP max-scan over LDS-marked wave-row starts and its position from
+// ballot prefix counts, 40 / 110 / 499 us against 38 / 112 / 427.  Timing-only
+// builds at k = 2^26: no output stores 294 us, stores folded onto L2-resident
+// slots 346, full 414.)
 template <typename F>
 __device__ __forceinline__ void tk5_entries(const int32_t *__restrict__ sv, const uint8_t *__restrict__ sp,
                                             uint32_t c, F &&f) {
