@@ -35,4 +35,13 @@ import json
 for l in open('$O/adv.jsonl'):
     d=json.loads(l); c=d['config']
     print(c.get('family', '?'), 'k', c.get('k'), round(d['value'],1), 'Gkeys/s', round(d['ms_per_step'],4), 'ms', 'path', d.get('path'), 'cands', d.get('candidates'), d['verified'])"
+echo "== rows (BASELINE config 5: uniform and duplicate-heavy, k-th and top-k)"
+for args in "--rows-dtype i32" "--rows-dtype f32" "--rows-dtype i32 --topk" "--rows-dtype f32 --topk" "--rows-dtype i32 --rows-input dup" "--rows-dtype f32 --rows-input dup"; do
+  timeout -k 10 120 python -u bench.py --workload rows $args --k 64 --steps 20 --warmup 3 >> $O/rows.jsonl 2>$O/rows.err || { echo "rows $args rc=$?"; tail -20 $O/rows.err; exit 1; }
+done
+python3 -c "
+import json
+for l in open('$O/rows.jsonl'):
+    d=json.loads(l); c=d['config']; r=d['roofline']
+    print(c['workload'], round(d['value'],1), 'Gkeys/s kernel', round(r['avg_launch_ms']*1e3,1), 'us frac', round(r['frac'],3), 'traffic', r['traffic'], d['verified'])"
 echo done

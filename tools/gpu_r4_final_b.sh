@@ -1,6 +1,7 @@
 # Round 4 evidence (b): PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE
-# passes) on the final build for the select, the rows and the staged top-k;
-# the 2^33 lines; the warmup transient with and without candidate staging.
+# passes) on the final build for the select, the rows (k-th and top-k) and the
+# staged top-k; the 2^33 lines; the SQ instruction mix of k_main and the rows
+# kernels.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/fb; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
 pmc2() {  # pmc2 NAME -- bench args: two passes, csv paths in $O/pmc_NAME_{FETCH,WRITE}_SIZE
@@ -41,10 +42,7 @@ for k in 1048576 67108864; do
   timeout -s KILL 120 rocprofv3 --pmc $C -d $O/sq_tk_$k -o run --output-format csv -- python3 bench.py --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_tk_$k.log 2>&1 || { echo sq rc=$?; tail -20 $O/sq_tk_$k.log; exit 1; }
   python3 tools/sq_mix.py $O/sq_tk_$k "k_main<5>" 1073741824 "top-k k=$k k_main<5>"
 done
-echo "== warmup transient: k_main per call, base vs no candidate staging (diagnostic build)"
-for v in base nostage0; do
-  lib=mpi-k-selection_amd/lib/variants/libkth_$v.so; [ $v = base ] && lib=mpi-k-selection_amd/lib/libkth.so
-  KTH_LIB=$PWD/$lib timeout -k 10 200 rocprofv3 --kernel-trace -d $O/bump_$v -o run --output-format csv -- python3 tools/bump_probe.py uniform_half > $O/bump_$v.log 2>&1 || { echo "bump $v rc=$?"; tail -20 $O/bump_$v.log; exit 1; }
-  echo "$v:"; python3 tools/prof_calls.py $(find $O/bump_$v -name "*kernel_trace.csv" | head -1) | grep "k_main" | cut -c1-420
-done
+echo "== SQ mix of the rows kernels per 64-key slot (k-th and top-k, i32 and f32)"
+timeout -k 10 600 bash tools/gpu_rows_pmc_sq.sh > $O/rows_sq.txt 2>&1 || { echo rows sq rc=$?; tail -20 $O/rows_sq.txt; exit 1; }
+cat $O/rows_sq.txt
 echo done
