@@ -350,6 +350,42 @@ __device__ __forceinline__ uint32_t vbin(float v, float s, float o) {
     return (uint32_t)__builtin_amdgcn_fmed3f(__builtin_fmaf(v, s, o), 0.f, 255.f);
 }
 
+// The kk-th of the keys in [amin, amin + 8) when that interval holds it (its
+// keys are the smallest kk or more of the range counted): every lane counts
+// its keys of each value in 8-bit fields of two registers (no LDS atomics),
+// one wave sum per pair of values in 16-bit fields.  kk becomes the rank among
+// the answer's equal keys, *eq_out their number.
+template <int KPL>
+__device__ __forceinline__ uint32_t row_count_small(const uint32_t (&key)[KPL], uint32_t amin, uint32_t &kk,
+                                                    uint32_t *eq_out) {
+    // value d = x - amin of every key in [amin, amin + 8): field d & 3 of c[d >> 2]
+    const uint32_t ob = opaque(amin);
+    uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const uint32_t d = key[j] - ob;
+        const uint32_t inc = 1u << ((d & 3u) << 3);
+        c0 += d < 4u ? inc : 0u;
+        c1 += d - 4u < 4u ? inc : 0u;
+    }
+    // (a lane counts <= KPL <= 64 keys a value: 8-bit fields; the wave sums in 16-bit fields)
+    const auto add = [](uint32_t a, uint32_t b) { return a + b; };
+    const uint32_t s01 = wave_reduce(c0 & 0x00FF00FFu, 0u, add), s23 = wave_reduce((c0 >> 8) & 0x00FF00FFu, 0u, add);
+    const uint32_t s45 = wave_reduce(c1 & 0x00FF00FFu, 0u, add), s67 = wave_reduce((c1 >> 8) & 0x00FF00FFu, 0u, add);
+    const uint32_t n[8] = {s01 & 0xFFFFu, s23 & 0xFFFFu, s01 >> 16, s23 >> 16,
+                           s45 & 0xFFFFu, s67 & 0xFFFFu, s45 >> 16, s67 >> 16};
+    uint32_t d = 0, acc = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (acc < kk) {  // wave-uniform
+            d = (uint32_t)q;
+            acc += n[q];
+        }
+    kk -= acc - n[d];
+    if (eq_out) *eq_out = n[d];
+    return amin + d;
+}
+
 // A picked bin of more than 64 keys (duplicate-heavy or clustered rows; was:
 // four masked 8-bit radix sweeps of the whole row, ~24-35 VALU ops and four
 // LDS atomics a key, and the atomics of a few-valued row serialise on a few
@@ -370,17 +406,46 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
                                                          uint32_t bin, uint32_t cnt, uint32_t *eq_out,
                                                          ToKeys &&to_keys) {
     uint32_t amin = 0xFFFFFFFFu, amax = 0u;
-    if (F32 && vmap) {  // key[] holds raw float bits: the bin test on the value, min / max on the order key
+    if (F32 && vmap) {  // key[] holds raw float bits
         const float s2 = opaque(fs);
         float o2;
         asm volatile("v_mov_b32 %0, %1" : "=v"(o2) : "s"(opaque(fo)));
         const uint32_t ob = opaque(bin), fl = opaque(flip);
+        // The bin's value range from float min / max (no order key per key):
+        // vbin(v) == B  <=>  lo <= fma(v, s, o) and !(fma >= hi), with lo = -inf
+        // for B = 0 and hi = NaN for B = 255 (the clamps); keys outside the bin
+        // enter as +-inf.
+        const float lo_t = ob == 0u ? -__builtin_inff() : (float)ob;
+        const float hi_t = ob == 255u ? __builtin_nanf("") : (float)(ob + 1u);
+        float vlo = __builtin_inff(), vhi = -__builtin_inff();
 #pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const bool in = vbin(__uint_as_float(key[j]), s2, o2) == ob;
-            const uint32_t u = key_of_f32(key[j]) ^ fl;
-            amin = in ? min(amin, u) : amin;
-            amax = in ? max(amax, u) : amax;
+        for (int j = 0; j < KPL; j += 2) {
+            const float a = __uint_as_float(key[j]), b = __uint_as_float(key[j + 1]);
+            const float ta = __builtin_fmaf(a, s2, o2), tb = __builtin_fmaf(b, s2, o2);
+            const bool ia = ta >= lo_t && !(ta >= hi_t), ib = tb >= lo_t && !(tb >= hi_t);
+            vlo = min3f(vlo, ia ? a : __builtin_inff(), ib ? b : __builtin_inff());
+            vhi = max3f(vhi, ia ? a : -__builtin_inff(), ib ? b : -__builtin_inff());
+        }
+        vlo = __uint_as_float(wave_reduce(__float_as_uint(vlo), 0x7F800000u, [](uint32_t x, uint32_t y) {
+            return __float_as_uint(min3f(__uint_as_float(x), __uint_as_float(y), __uint_as_float(y)));
+        }));
+        vhi = __uint_as_float(wave_reduce(__float_as_uint(vhi), 0xFF800000u, [](uint32_t x, uint32_t y) {
+            return __float_as_uint(max3f(__uint_as_float(x), __uint_as_float(y), __uint_as_float(y)));
+        }));
+        if (vlo != 0.f && vhi != 0.f) {  // wave-uniform
+            const uint32_t klo = key_of_f32(__float_as_uint(vlo)) ^ fl, khi = key_of_f32(__float_as_uint(vhi)) ^ fl;
+            amin = fl ? khi : klo;
+            amax = fl ? klo : khi;
+        } else {
+            // a zero at an end: min / max do not see its sign (-0 < +0 as
+            // keys), so the ends are taken on the order keys
+#pragma unroll
+            for (int j = 0; j < KPL; ++j) {
+                const bool in = vbin(__uint_as_float(key[j]), s2, o2) == ob;
+                const uint32_t u = key_of_f32(key[j]) ^ fl;
+                amin = in ? min(amin, u) : amin;
+                amax = in ? max(amax, u) : amax;
+            }
         }
         to_keys();
     } else {
@@ -399,34 +464,7 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
         if (eq_out) *eq_out = cnt;
         return amin;
     }
-    if (span < 8) {
-        // value d = x - amin of every key in [amin, amax]: field d & 3 of c[d >> 2]
-        const uint32_t ob = opaque(amin);
-        uint32_t c0 = 0, c1 = 0;
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const uint32_t d = key[j] - ob;
-            const uint32_t inc = 1u << ((d & 3u) << 3);
-            c0 += d < 4u ? inc : 0u;
-            c1 += d - 4u < 4u ? inc : 0u;
-        }
-        // (a lane counts <= KPL <= 64 keys a value: 8-bit fields; the wave sums in 16-bit fields)
-        const auto add = [](uint32_t a, uint32_t b) { return a + b; };
-        const uint32_t s01 = wave_reduce(c0 & 0x00FF00FFu, 0u, add), s23 = wave_reduce((c0 >> 8) & 0x00FF00FFu, 0u, add);
-        const uint32_t s45 = wave_reduce(c1 & 0x00FF00FFu, 0u, add), s67 = wave_reduce((c1 >> 8) & 0x00FF00FFu, 0u, add);
-        const uint32_t n[8] = {s01 & 0xFFFFu, s23 & 0xFFFFu, s01 >> 16, s23 >> 16,
-                               s45 & 0xFFFFu, s67 & 0xFFFFu, s45 >> 16, s67 >> 16};
-        uint32_t d = 0, acc = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (acc < kk) {  // wave-uniform
-                d = (uint32_t)q;
-                acc += n[q];
-            }
-        kk -= acc - n[d];
-        if (eq_out) *eq_out = n[d];
-        return amin + d;
-    }
+    if (span < 8) return row_count_small<KPL>(key, amin, kk, eq_out);
     // wider intervals (clustered rows; rare): the masked radix sweeps of the row
     const uint32_t ans = row_select_radix<KPL, 4>(key, hist, lane, kk_row);
     kk = kk_row;
@@ -519,6 +557,30 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
         fs = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fs)));
         fo = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(fo)));
         if (!vmap) to_keys();
+    }
+    if constexpr (!F32) {
+        // Few-valued int rows (BASELINE config 5's duplicate-heavy variant):
+        // their top-byte histogram sends a whole wave's keys to one or two LDS
+        // addresses, and the atomics serialise (~2x the row's time).  When the
+        // first key slot holds at most two top bytes (~never for spread-out
+        // rows: three wave-uniform tests), the row's range decides: within 8
+        // values the answer is counted in registers, no histogram at all.
+        const uint32_t t0 = key[0] >> 24, b0 = __builtin_amdgcn_readfirstlane(t0);
+        unsigned long long mm = __ballot(t0 == b0);
+        if (~mm != 0ull) {  // wave-uniform
+            const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)t0, __builtin_ctzll(~mm));
+            mm |= __ballot(t0 == b1);
+        }
+        if (mm == ~0ull) {  // wave-uniform
+            uint32_t lmin = key[0], lmax = key[0];
+#pragma unroll
+            for (int j = 1; j < KPL; ++j) {
+                lmin = min(lmin, key[j]);
+                lmax = max(lmax, key[j]);
+            }
+            const uint32_t kmin = wave_min_u32(lmin), kmax = wave_max_u32(lmax);
+            if (kmax - kmin < 8u) return row_count_small<KPL>(key, kmin, kk, eq_out);
+        }
     }
     zero_hist(hist, R0, lane);
     __builtin_amdgcn_wave_barrier();
