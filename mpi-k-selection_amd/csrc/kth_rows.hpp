@@ -432,19 +432,47 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
         vhi = __uint_as_float(wave_reduce(__float_as_uint(vhi), 0xFF800000u, [](uint32_t x, uint32_t y) {
             return __float_as_uint(max3f(__uint_as_float(x), __uint_as_float(y), __uint_as_float(y)));
         }));
-        if (vlo != 0.f && vhi != 0.f) {  // wave-uniform
-            const uint32_t klo = key_of_f32(__float_as_uint(vlo)) ^ fl, khi = key_of_f32(__float_as_uint(vhi)) ^ fl;
-            amin = fl ? khi : klo;
-            amax = fl ? klo : khi;
-        } else {
-            // a zero at an end: min / max do not see its sign (-0 < +0 as
-            // keys), so the ends are taken on the order keys
+        // the ends as order keys; an end at zero does not tell its sign (min /
+        // max see -0 == +0, the keys -0 < +0): the zeros present stand in for
+        // it (every zero of the row is in this bin then: one value, one bin)
+        auto end_key = [&](float v) { return key_of_f32(__float_as_uint(v)) ^ fl; };
+        if (vlo != 0.f) {
+            amin = min(amin, end_key(vlo));
+            amax = max(amax, end_key(vlo));
+        }
+        if (vhi != 0.f) {
+            amin = min(amin, end_key(vhi));
+            amax = max(amax, end_key(vhi));
+        }
+        if (vlo == 0.f || vhi == 0.f) {  // wave-uniform
+            uint32_t nz = 0, pz = 0;  // this lane's -0.0 / +0.0 keys
 #pragma unroll
             for (int j = 0; j < KPL; ++j) {
-                const bool in = vbin(__uint_as_float(key[j]), s2, o2) == ob;
-                const uint32_t u = key_of_f32(key[j]) ^ fl;
-                amin = in ? min(amin, u) : amin;
-                amax = in ? max(amax, u) : amax;
+                nz += key[j] == 0x80000000u ? 1u : 0u;
+                pz += key[j] == 0u ? 1u : 0u;
+            }
+            const auto add = [](uint32_t a, uint32_t b) { return a + b; };
+            const uint32_t cn = wave_reduce(nz, 0u, add), cp = wave_reduce(pz, 0u, add);
+            const uint32_t kn = end_key(-0.0f), kp = end_key(0.0f);
+            if (cn) {
+                amin = min(amin, kn);
+                amax = max(amax, kn);
+            }
+            if (cp) {
+                amin = min(amin, kp);
+                amax = max(amax, kp);
+            }
+            if (cn && cp && amin == min(kn, kp) && amax == max(kn, kp)) {
+                // the bin is the two zeros: the kk-th from their counts
+                const uint32_t c1 = amin == kn ? cn : cp, c2 = amin == kn ? cp : cn;
+                to_keys();
+                if (kk <= c1) {
+                    if (eq_out) *eq_out = c1;
+                    return amin;
+                }
+                kk -= c1;
+                if (eq_out) *eq_out = c2;
+                return amax;
             }
         }
         to_keys();
