@@ -25,6 +25,10 @@ constexpr int RW_BLOCK = 256;
 #define KTH_TOPK_RELOAD 1
 #endif
 constexpr bool TOPK_RELOAD = KTH_TOPK_RELOAD;  // top-k compaction re-reads full rows from L2
+#ifndef KTH_TOPK_KEYS_COMPACT
+#define KTH_TOPK_KEYS_COMPACT 1
+#endif
+constexpr bool TOPK_KEYS_COMPACT = KTH_TOPK_KEYS_COMPACT;  // unstaged full top-k rows compact from key[]
 #ifndef KTH_TOPK_NT
 #define KTH_TOPK_NT 1  // top-k rows load with the non-temporal hint too (the staged path reads a row once)
 #endif
@@ -1004,7 +1008,19 @@ __global__ __launch_bounds__(RW_BLOCK, !VEC ? 1 : (TOPK && !(TOPK_RELOAD && FULL
                 }
             };
             const bool all_ties = FULL && kk == eqn;
-            if (TOPK_RELOAD && FULL && all_ties) {
+            if (TOPK_KEYS_COMPACT && !F32 && TOPK_RELOAD && FULL) {
+                // int rows: key[] still holds the row's order keys (KEYS_OUT):
+                // compact from the registers -- the re-read below comes from HBM
+                // (the row was loaded non-temporal), a second pass over the
+                // row's bytes.  (Float rows: the same code made the kernel
+                // spill 200 B in its prologue.)
+#pragma unroll
+                for (int j = 0; j < KPL / 4; ++j) {
+                    const uint32_t g[4] = {key[4 * j], key[4 * j + 1], key[4 * j + 2], key[4 * j + 3]};
+                    group((uint32_t)(j * WAVE + lane) * 4u, g);
+                    __builtin_amdgcn_sched_barrier(0);  // keep the groups apart: no hoisting across them (VGPRs)
+                }
+            } else if (TOPK_RELOAD && FULL && all_ties) {
                 // the row again, from L2, every group's load in flight at once (the
                 // keys' registers are free by now): one round trip per row, not
                 // one per two groups
