@@ -658,3 +658,82 @@ def test_topk_rows_many_rows(gpu, f32):
         gpu.sync()
         assert torch.equal(idx, want), largest
         assert torch.equal(vals.view(torch.int32), torch.gather(m, 1, want.to(torch.int64)).view(torch.int32)), largest
+
+
+def _few_valued_rows(rng, rows, cols, f32):
+    """Rows for the few-valued int path (<= 8 values, no histogram) and the
+    dense float bin whose ends are zeros: values at INT_MIN / INT_MAX, two
+    top bytes in the first key slot with a wide rest, -0.0 / +0.0 mixes."""
+    m = np.empty((rows, cols), dtype=np.float32 if f32 else np.int32)
+    for i in range(rows):
+        f = i % 8
+        if f32:
+            if f == 0:
+                m[i] = np.round(rng.uniform(-1, 1, cols) * 8) / 8                 # 17 values, both zeros
+            elif f == 1:
+                m[i] = rng.choice(np.array([-0.0, 0.0, 0.5], dtype=np.float32), cols)
+            elif f == 2:
+                m[i] = rng.choice(np.array([-0.0, 0.0], dtype=np.float32), cols)
+                m[i, int(rng.integers(cols))] = -3.0                              # range > 0: value-linear bins
+            elif f == 3:
+                m[i] = rng.choice(np.array([-2.0, -0.0, 0.0, 1e-30], dtype=np.float32), cols)
+            elif f == 4:
+                m[i] = np.round(rng.normal(0, 1, cols) * 2) / 2
+            elif f == 5:
+                m[i] = rng.choice(np.array([-1.0, -0.0], dtype=np.float32), cols)
+            elif f == 6:
+                m[i] = rng.choice(np.array([0.0, 7.0], dtype=np.float32), cols)
+            else:
+                m[i] = rng.uniform(-1, 1, cols)
+        else:
+            if f == 0:
+                m[i] = rng.integers(-1, 1, cols)                                  # {-1, 0}: two top bytes
+            elif f == 1:
+                m[i] = rng.integers(-2 ** 31, -2 ** 31 + 8, cols)                 # 8 values at INT_MIN
+            elif f == 2:
+                m[i] = rng.integers(2 ** 31 - 8, 2 ** 31, cols)                   # 8 values at INT_MAX
+            elif f == 3:
+                m[i] = rng.integers(0, 9, cols)                                   # 9 values: one too many
+                m[i, :4 * 64] = 0                                                 # (first slot: one top byte)
+            elif f == 4:
+                m[i] = rng.integers(-2 ** 31, 2 ** 31, cols)
+                m[i, :4 * 64] = 5                                                 # few-valued slot, wide row
+            elif f == 5:
+                m[i] = 42
+            elif f == 6:
+                m[i] = rng.integers(1000, 1008, cols)
+            else:
+                m[i] = rng.integers(-2 ** 31, 2 ** 31, cols)
+    return m
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_rows_few_valued_and_zero_bins(gpu, f32):
+    """k-th and top-k per row (smallest and largest) on rows for the
+    few-valued int path and the dense float bin with zero ends (round 4)."""
+    import torch
+    rows, cols = 160, 4096
+    rng = np.random.default_rng(4321 + f32)
+    m = _few_valued_rows(rng, rows, cols, f32)
+    d = torch.from_numpy(m).cuda()
+    keys = _f32_order_key(m).astype(np.int64) if f32 else m.astype(np.int64)
+    out = torch.empty(rows, dtype=torch.float32 if f32 else torch.int32, device="cuda")
+    for k in (1, 2, 64, 1000, 2047, 2048, 2049, 4095, 4096):
+        gpu.rows(d, rows, cols, k, out, f32=f32)
+        gpu.sync()
+        want = m[np.arange(rows), np.argsort(keys, axis=1, kind="stable")[:, k - 1]]
+        got = out.cpu().numpy()
+        if f32:
+            np.testing.assert_array_equal(_f32_order_key(got), _f32_order_key(want), err_msg=f"k={k}")
+        else:
+            np.testing.assert_array_equal(got, want, err_msg=f"k={k}")
+    for k in (1, 64, 2048, 4096):
+        for largest in (False, True):
+            vals = torch.empty((rows, k), dtype=out.dtype, device="cuda")
+            idx = torch.empty((rows, k), dtype=torch.int32, device="cuda")
+            gpu.topk_rows(d, rows, cols, k, vals, idx, largest=largest, f32=f32)
+            gpu.sync()
+            want_idx = _topk_ref(keys, k, largest)
+            np.testing.assert_array_equal(idx.cpu().numpy(), want_idx, err_msg=f"topk k={k} largest={largest}")
+            np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32),
+                                          np.take_along_axis(m, want_idx, axis=1).view(np.uint32))
