@@ -63,29 +63,38 @@ def cpu_model():
     return platform.processor()
 
 
-def _free_port():
-    import socket
+RDV_ENV = "KTH_RDV_FILE"  # launch_ranks' file rendezvous (no TCP port to probe and race for)
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+
+def init_group(dev, backend="nccl"):
+    """The ranks' process group: under torchrun (the driver's launch) env://
+    with the launcher's store; under launch_ranks a FileStore at $KTH_RDV_FILE."""
+    import torch.distributed as dist
+
+    path = os.environ.get(RDV_ENV)
+    if path:
+        dist.init_process_group(backend, device_id=dev, init_method="file://" + path,
+                                rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+    else:
+        dist.init_process_group(backend, device_id=dev)
 
 
 def launch_ranks(n, argv):
     """`bench.py --gpus N` without a launcher: start N rank processes of this
-    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, one
-    GPU each), replacing the reference's `mpirun -n P` launch
-    (TODO-kth-problem-cgm.c:53-61).  This parent never imports torch or touches a
-    GPU; it forwards the ranks' output, stops every rank when one fails, and
-    exits with the first failing rank's code."""
-    port = _free_port()
-    log(f"bench: launching {n} ranks (one per GPU), rendezvous 127.0.0.1:{port}")
+    script (RANK / LOCAL_RANK / WORLD_SIZE set, one GPU each, rendezvous through
+    a FileStore file named by $KTH_RDV_FILE: no port is probed, so none can be
+    taken between the probe and the bind), replacing the reference's
+    `mpirun -n P` launch (TODO-kth-problem-cgm.c:53-61).  This parent never
+    imports torch or touches a GPU; it forwards the ranks' output, stops every
+    rank when one fails, and exits with the first failing rank's code."""
+    rdv_dir = tempfile.mkdtemp(prefix="kth_rdv_")
+    rdv = os.path.join(rdv_dir, "store")
+    log(f"bench: launching {n} ranks (one per GPU), rendezvous file://{rdv}")
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", **{RDV_ENV: rdv})
+        env.pop("MASTER_PORT", None)
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
     rc = 0
     live = list(enumerate(procs))
@@ -102,6 +111,9 @@ def launch_ranks(n, argv):
                 rc = rc or code
                 for _, q in live:
                     q.terminate()
+    for f in os.listdir(rdv_dir):
+        os.unlink(os.path.join(rdv_dir, f))
+    os.rmdir(rdv_dir)
     return rc
 
 
@@ -277,7 +289,7 @@ def rows_main(args):
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_group(dev)
     sel = kselect.Selector(local_rank, stream=stream)
     R, C = args.rows, args.cols
     k = args.k or C // 2
@@ -402,7 +414,7 @@ def topk_main(args):
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_group(dev)
     sel = kselect.Selector(local_rank, stream=stream)
     n = 1 << args.log2n
     k = args.k or 1024
@@ -486,6 +498,9 @@ def main():
                     help="rows workload input: uniform (f32 U(-1,1), int32 full range) or dup (duplicate-heavy)")
     ap.add_argument("--probe-launch", action="store_true",
                     help="(tests) each rank prints its launch environment as JSON and exits before touching a GPU")
+    ap.add_argument("--probe-rendezvous", action="store_true",
+                    help="(tests) the ranks meet as a gloo group through the launch's rendezvous, all-reduce their "
+                         "ranks and print the sum; no GPU is touched")
     args = ap.parse_args()
     if args.gpus < 1:
         log(f"bench: --gpus {args.gpus} must be >= 1")
@@ -496,8 +511,18 @@ def main():
     if world != args.gpus:
         log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run as {args.gpus}")
         return 2
+    if args.probe_rendezvous:
+        import torch
+        import torch.distributed as dist
+
+        init_group(None, backend="gloo")
+        t = torch.tensor([int(os.environ.get("RANK", 0))])
+        dist.all_reduce(t)
+        emit({"rank": dist.get_rank(), "world": dist.get_world_size(), "rank_sum": int(t.item())})
+        dist.destroy_process_group()
+        return 0
     if args.probe_launch:
-        emit({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")})
+        emit({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", RDV_ENV)})
         return 0
     if args.workload == "rows":
         return rows_main(args)
@@ -519,7 +544,7 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(dev))
     sharded = world > 1 or args.dist
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_group(dev)
     elif args.dist:  # the sharded protocol on one GPU: a one-rank RCCL group
         dist.init_process_group("nccl", device_id=dev, store=dist.HashStore(), rank=0, world_size=1)
 

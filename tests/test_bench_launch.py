@@ -18,7 +18,8 @@ BENCH = os.path.join(REPO, "bench.py")
 
 
 def _run(args, env_extra=None, timeout=180):
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "KTH_RDV_FILE")}
     env.update(env_extra or {})
     return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=env,
                           cwd="/tmp")
@@ -33,8 +34,22 @@ def test_launcher_spawns_n_ranks(n):
     assert {x["WORLD_SIZE"] for x in ranks} == {str(n)}
     assert sorted(int(x["LOCAL_RANK"]) for x in ranks) == list(range(n))
     assert {x["MASTER_ADDR"] for x in ranks} == {"127.0.0.1"}
-    assert len({x["MASTER_PORT"] for x in ranks}) == 1
+    # one shared FileStore rendezvous, no probed TCP port (round 4's EADDRINUSE)
+    assert {x["MASTER_PORT"] for x in ranks} == {None}
+    rdv = {x["KTH_RDV_FILE"] for x in ranks}
+    assert len(rdv) == 1 and rdv.pop().startswith("/")
     assert f"launching {n} ranks" in r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_rendezvous(n):
+    """The ranks launch_ranks starts really meet through its file rendezvous
+    (the same init_group the nccl ranks use, on gloo here) and all-reduce."""
+    r = _run(["--gpus", str(n), "--probe-rendezvous"])
+    assert r.returncode == 0, r.stderr
+    out = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert sorted(x["rank"] for x in out) == list(range(n))
+    assert {(x["world"], x["rank_sum"]) for x in out} == {(n, n * (n - 1) // 2)}
 
 
 def test_world_size_mismatch_refused():

@@ -8,8 +8,8 @@ TODO-kth-problem-cgm.c:81-100), across families, edge ranks, ragged shards and
 the window-fallback path.
 """
 import os
-import socket
 import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -18,19 +18,15 @@ import torch.multiprocessing as mp
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rdv():
+    """A fresh file:// rendezvous: the ranks meet through a FileStore, so no TCP
+    port is probed and then raced for (round 4's EADDRINUSE)."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="kth_rdv_"), "store")
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, rdv, cases, q):
     sys.path.insert(0, HERE)
     from conftest import PKG  # noqa: F401 -- sets sys.path for kselect and gen
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import torch
     import torch.distributed as dist
 
@@ -38,7 +34,7 @@ def _worker(rank, world, port, cases, q):
     from dist_cpu_backend import CpuBackend
     from kselect.dist import DistSelector, shard_bounds
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         out = []
         for fam, param, n, ks, cap in cases:
@@ -57,8 +53,8 @@ def _worker(rank, world, port, cases, q):
 def _run(world, cases):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    rdv = _rdv()
+    procs = [ctx.Process(target=_worker, args=(r, world, rdv, cases, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -117,18 +113,16 @@ def test_dist_selector_gloo_fallback():
     assert paths == {"fallback"}
 
 
-def _bad_worker(rank, world, port, q):
+def _bad_worker(rank, world, rdv, q):
     sys.path.insert(0, HERE)
     from conftest import PKG  # noqa: F401
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import torch
     import torch.distributed as dist
 
     from dist_cpu_backend import CpuBackend
     from kselect.dist import DistSelector
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         ds = DistSelector(CpuBackend())
         errs = []
@@ -153,8 +147,8 @@ def _bad_worker(rank, world, port, q):
 def test_dist_selector_bad_arguments_raise_on_every_rank():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_bad_worker, args=(r, 2, port, q)) for r in range(2)]
+    rdv = _rdv()
+    procs = [ctx.Process(target=_bad_worker, args=(r, 2, rdv, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(2))

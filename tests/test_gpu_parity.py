@@ -6,8 +6,6 @@ Sizes: golden fixtures (reference outputs, n <= 16384); synthetic families up to
 certificate #(<v) < k <= #(<=v), which holds iff v is the k-th smallest.
 """
 import ctypes
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -539,22 +537,14 @@ def test_topk_rows_errors(gpu):
 
 
 # ----------------------------------------------------- sharded, one rank
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def test_dist_world1_nccl(gpu):
     """The sharded protocol (kth_dist_* + RCCL collectives) with one rank."""
     import torch
     import torch.distributed as dist
     from kselect.dist import DistSelector, HipBackend
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    # one rank over an in-process HashStore: no TCP port to race for
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0),
+                            store=dist.HashStore())
     try:
         from kselect.rccl import RcclComm, TorchComm
         b = HipBackend(0)

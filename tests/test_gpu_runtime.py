@@ -18,7 +18,6 @@
 """
 import contextlib
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -28,21 +27,14 @@ from conftest import load_input
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @contextlib.contextmanager
 def _world1():
+    """A one-rank RCCL group over an in-process HashStore: no TCP rendezvous, so
+    no port to race for (round 4's driver run lost a probed port to EADDRINUSE)."""
     import torch
     import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0),
+                            store=dist.HashStore())
     try:
         yield
     finally:
