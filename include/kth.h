@@ -101,6 +101,12 @@ int kth_select_i32_async(kth_ctx *ctx, const int32_t *d_keys, int64_t n, int64_t
 /* Stats of the last select on this ctx (synchronises the ctx stream). */
 int kth_ctx_last_stats(kth_ctx *ctx, kth_stats *st);
 
+/* Diagnostics: 1 when the ctx runs the cooperative (grid-barrier) kernels,
+ * 0 while it is on the per-level path -- for COOP_BACKOFF = 64 selections of
+ * any entry point after a grid-barrier timeout (the synchronous entry points
+ * redo the timed-out select; the asynchronous ones report it in the stats). */
+int kth_ctx_coop(const kth_ctx *ctx);
+
 /* --- timing (bench) ----------------------------------------------------------
  * When enabled, every select records HIP events on the ctx stream around the
  * streaming pass (the dominant kernel) and around the whole select. */
@@ -160,28 +166,38 @@ int kth_fill_synthetic(kth_ctx *ctx, int32_t *d_out, int64_t n, int64_t offset, 
  * :139-165, Bcast :168, 3-way count :171-185, Allreduce :190, discard
  * :194-225, final Gatherv + sort :242-278) become:
  *   every rank samples its shard -> the samples are all-gathered -> every rank
- *   derives the same window -> one streaming pass per shard (counts + local
- *   candidates) -> per-rank histograms are all-reduced (uint64 SUM) after each
- *   step -> every rank picks the same digit from the same reduced histogram.
+ *   derives the same window -> one streaming pass per shard (counts, local
+ *   candidates and their first digit) -> per-rank histograms are all-reduced
+ *   (uint64 SUM) after each step -> every rank picks the same digit from the
+ *   same reduced histogram.
+ * Collectives per selection: one all-gather and, when the window is at most
+ * 2^24 key values wide (uniform 2^33 half-range keys: ~2^23.3), two
+ * all-reduces; wider windows three; the exact fallback after a window miss or
+ * a candidate overflow four; a selection decided by the window's counts alone
+ * two (the second all-reduce carries an empty slot).
  * The host owns the collectives (RCCL through torch.distributed in
  * kselect/dist.py, or MPI/RCCL from C); these entry points only enqueue the
- * per-rank device work on the ctx stream and never synchronise the host.
+ * per-rank device work on the ctx stream.  The host waits once per selection:
+ * kth_dist_level(1) waits for level 0's kernel (the device has the all-reduce
+ * after it still queued) to learn how many levels follow.
  *
  * d_slots: caller-owned device memory of 3 * KTH_STATS_WORDS uint64 words,
  * bound by kth_dist_begin for one selection.  kth_dist_scan and
  * kth_dist_level return the index (0..2) of the slot the caller must
- * all-reduce (SUM) in place across ranks before the next call; every rank
- * must make the same sequence of calls.
- *   kth_dist_begin   bind slots, zero them, set (n_total, k)
+ * all-reduce (SUM) in place across ranks before the next call, or
+ * KTH_DIST_DONE; every rank makes the same sequence of calls:
+ *   kth_dist_begin   bind slots, set (n_total, k)
  *   kth_dist_sample  local sample of s_local keys of the shard -> d_sample
  *                    (order-preserving uint32 keys); caller all-gathers
  *   kth_dist_window  window from the gathered sample of s_total keys
  *   kth_dist_scan    streaming pass over the shard            -> slot
- *   kth_dist_level   level = 0 .. KTH_DIST_LEVELS-1           -> slot
+ *   kth_dist_level   level = 0, 1, 2, ... -> slot, until it returns
+ *                    KTH_DIST_DONE (at most KTH_DIST_MAX_LEVELS slots)
  *   kth_dist_result  writes the k-th smallest of the union of all shards to
  *                    *d_out (device) */
 #define KTH_STATS_WORDS (8 + 2 * 2048)
-#define KTH_DIST_LEVELS 3
+#define KTH_DIST_DONE 3
+#define KTH_DIST_MAX_LEVELS 3
 int kth_dist_begin(kth_ctx *ctx, uint64_t *d_slots, int64_t n_total, int64_t k);
 int kth_dist_sample(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, uint32_t *d_sample,
                     int64_t s_local);

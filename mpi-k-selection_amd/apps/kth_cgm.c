@@ -8,7 +8,11 @@
  *   - the block partition sizev[i] = n/P + (i < n%P) and MPI_Scatterv of the
  *     keys from rank 0 (:81-105);
  *   - MPI_Wtime from before the scatter to the answer (:76, :279) and rank 0's
- *     output line "kth element=%d \ntime: %f\n" (:280);
+ *     output lines: "kth element %d\n time: %f\n" (:289) when the answer is
+ *     a window edge decided from the all-reduced counts (the reference's pivot
+ *     found by its 3-way count, :194-201), else "kth element=%d \ntime: %f\n"
+ *     (:280, the answer resolved from the candidates, as the reference's
+ *     final gather + sort);
  *   - k is 1-based (VecGet(pVec, k - 1), :278).
  * Replaced: the local qsort (:115), the weighted-median rounds (:122-233) and
  * the final Gather/Gatherv + rank-0 sort (:235-278).  Each rank copies its shard
@@ -97,10 +101,14 @@ static void allgather_sample(comm_t *c, const uint32_t *d_sample, uint32_t *d_al
     HIPCHK(hipMemcpyAsync(d_all, c->h_sample_all, (size_t)s * 4 * P, hipMemcpyHostToDevice, c->stream));
 }
 
-/* One sharded select of global rank k over every rank's d_keys[0..n_local). */
+/* One sharded select of global rank k over every rank's d_keys[0..n_local).
+ * *by_counts: the answer is a window edge, decided from the all-reduced counts
+ * alone -- the analogue of the reference's pivot found by its 3-way count
+ * (TODO-kth-problem-cgm.c:194-201, printed as :289); otherwise it was
+ * resolved from the candidates' digits (the final gather + solve, :235-280). */
 static int32_t dist_select(kth_ctx *ctx, comm_t *c, const int32_t *d_keys, int64_t n_local, int64_t n, int64_t k,
                            int P, uint64_t *d_slots, uint32_t *d_sample, uint32_t *d_sample_all, int64_t s,
-                           int32_t *d_answer)
+                           int32_t *d_answer, int *by_counts)
 {
     KTHCHK(kth_dist_begin(ctx, d_slots, n, k));
     KTHCHK(kth_dist_sample(ctx, d_keys, n_local, d_sample, s));
@@ -109,12 +117,18 @@ static int32_t dist_select(kth_ctx *ctx, comm_t *c, const int32_t *d_keys, int64
     int slot = kth_dist_scan(ctx, d_keys, n_local);
     KTHCHK(slot);
     allreduce_slot(c, d_slots, slot);
-    for (int l = 0; l < KTH_DIST_LEVELS; ++l) {
+    for (int l = 0;; ++l) { /* usually one level: two all-reduces in all */
         slot = kth_dist_level(ctx, d_keys, n_local, l);
         KTHCHK(slot);
+        if (slot == KTH_DIST_DONE) break;
         allreduce_slot(c, d_slots, slot);
     }
     KTHCHK(kth_dist_result(ctx, d_answer));
+    kth_stats st;
+    KTHCHK(kth_ctx_last_stats(ctx, &st)); /* synchronises the stream */
+    if (st.error != 0) DIE("sharded select: device error %d", st.error);
+    const uint32_t key = (uint32_t)st.answer ^ 0x80000000u;
+    if (by_counts) *by_counts = st.path == KTH_PATH_WINDOW && (key == st.lo_key || key == st.hi_key);
     int32_t ans = 0;
     HIPCHK(hipMemcpyAsync(&ans, d_answer, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -221,6 +235,7 @@ int main(int argc, char **argv)
     HIPCHK(hipMemcpyAsync(d_keys, h_local, (size_t)n_local * 4, hipMemcpyHostToDevice, c.stream));
 
     int32_t answer;
+    int by_counts = 0;
     /* Shards too small to sample (fewer than 64 keys on some rank): gather to
      * rank 0 and select there, as the reference's final step does (:235-278). */
     const int small = n / P < 64;
@@ -247,17 +262,24 @@ int main(int argc, char **argv)
             c.h_sample = (uint32_t *)malloc((size_t)s * 4);
             c.h_sample_all = (uint32_t *)malloc((size_t)s * 4 * P);
         }
-        answer = dist_select(ctx, &c, d_keys, n_local, n, k, P, d_slots, d_sample, d_sample_all, s, d_answer);
+        answer = dist_select(ctx, &c, d_keys, n_local, n, k, P, d_slots, d_sample, d_sample_all, s, d_answer,
+                             &by_counts);
     }
     double t1 = MPI_Wtime();
-    if (rank == 0) printf("kth element=%d \ntime: %f\n", answer, t1 - t0); /* :280 */
+    if (rank == 0) {
+        if (by_counts) /* the answer is a pivot the 3-way count found (:194-201) */
+            printf("kth element %d\n time: %f\n", answer, t1 - t0); /* :289 */
+        else
+            printf("kth element=%d \ntime: %f\n", answer, t1 - t0); /* :280 */
+    }
 
     /* device-resident repeats: the select alone, keys already in HBM */
     if (repeat > 0 && !small) {
         MPI_Barrier(MPI_COMM_WORLD);
         double r0 = MPI_Wtime();
         for (int r = 0; r < repeat; ++r) {
-            int32_t a = dist_select(ctx, &c, d_keys, n_local, n, k, P, d_slots, d_sample, d_sample_all, s, d_answer);
+            int32_t a = dist_select(ctx, &c, d_keys, n_local, n, k, P, d_slots, d_sample, d_sample_all, s, d_answer,
+                                    NULL);
             if (a != answer) DIE("repeat %d: answer %d differs from %d", r, a, answer);
         }
         MPI_Barrier(MPI_COMM_WORLD);

@@ -10,29 +10,76 @@
  * VecKthSelectEx(pVec, k, &solution), i.e. the GPU selection through the
  * C-ABI, with an explicit status instead of VecGet's in-band sentinels.
  *
- * Usage: kth_seq [n=100000000] [k=250] [seed=time(NULL)] [--median]
- *   --median sets k = n/2 as in kth-problem-seq.c~:24.
+ * Usage: kth_seq [n=100000000] [k=250] [seed=time(NULL)] [--median] [--breakdown]
+ *   --median    sets k = n/2 as in kth-problem-seq.c~:24.
+ *   --breakdown after the drop-in select, times its parts on a fresh ctx
+ *               (stderr, one JSON line): ctx creation, device allocation, the
+ *               host-to-device copy of the keys, the first and a second
+ *               select of the device-resident keys.
  * The reference times with clock() (CPU time, :30,35); this driver reports
  * the wall time of the select (the work happens on the GPU, so CPU time would
- * understate it) plus the same clock() figure on stderr.
+ * understate it) plus the same clock() figure on stderr.  That wall time is
+ * end to end: the drop-in's first call creates the HIP runtime and its ctx,
+ * stages the host keys to the device and selects.
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include "kth.h"
 #include "vector.h"
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* The drop-in's one-shot cost, part by part, on a fresh ctx (the HIP runtime
+ * is already up: the drop-in call created it). */
+static int breakdown(const int *keys, long n, long k, int expect)
+{
+    kth_ctx *ctx = NULL;
+    int32_t *d = NULL, a1 = 0, a2 = 0;
+    double t0 = now_s();
+    if (kth_ctx_create(0, &ctx) != KTH_OK) return 1;
+    double t1 = now_s();
+    if (kth_ctx_reserve(ctx, n) != KTH_OK || hipMalloc((void **)&d, (size_t)n * 4) != hipSuccess) return 1;
+    double t2 = now_s();
+    if (hipMemcpy(d, keys, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) return 1;
+    double t3 = now_s();
+    if (kth_select_i32_ctx(ctx, d, n, k, &a1) != KTH_OK) return 1;
+    double t4 = now_s();
+    if (kth_select_i32_ctx(ctx, d, n, k, &a2) != KTH_OK) return 1;
+    double t5 = now_s();
+    fprintf(stderr,
+            "{\"breakdown\": true, \"n\": %ld, \"k\": %ld, \"ctx_create_s\": %.6f, \"alloc_s\": %.6f, "
+            "\"h2d_s\": %.6f, \"h2d_gbs\": %.2f, \"select_first_s\": %.6f, \"select_second_s\": %.6f, "
+            "\"answers_agree\": %s}\n",
+            n, k, t1 - t0, t2 - t1, t3 - t2, (double)n * 4 / (t3 - t2) / 1e9, t4 - t3, t5 - t4,
+            (a1 == expect && a2 == expect) ? "true" : "false");
+    hipFree(d);
+    kth_ctx_destroy(ctx);
+    return (a1 == expect && a2 == expect) ? 0 : 3;
+}
 
 int main(int argc, char **argv)
 {
     long n = 100000000;
     long k = 250;
     unsigned seed = (unsigned)time(NULL);
-    int median = 0, pos = 0;
+    int median = 0, pos = 0, split = 0;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--median")) {
             median = 1;
+            continue;
+        }
+        if (!strcmp(argv[i], "--breakdown")) {
+            split = 1;
             continue;
         }
         long v = atol(argv[i]);
@@ -72,14 +119,17 @@ int main(int argc, char **argv)
     const int rc = VecKthSelectEx(pVec, (int)k, &solution);
     clock_gettime(CLOCK_MONOTONIC, &w1);
     clock_t end = clock();
-    VecDelete(pVec);
     if (rc != 0) {
+        VecDelete(pVec);
         fprintf(stderr, "kth_seq: select failed: %s (no CPU fallback)\n", kth_strerror(rc));
         return 1;
     }
 
     double wall = (double)(w1.tv_sec - w0.tv_sec) + 1e-9 * (double)(w1.tv_nsec - w0.tv_nsec);
     printf("Solution found solution=%d \ntime: %f\n", solution, wall);
+    fflush(stdout);
     fprintf(stderr, "cpu time (clock): %f\n", (end - start) / (double)CLOCKS_PER_SEC);
-    return 0;
+    const int brc = split ? breakdown(pVec->data, n, k, solution) : 0;
+    VecDelete(pVec);
+    return brc;
 }

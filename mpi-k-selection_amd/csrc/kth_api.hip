@@ -66,6 +66,7 @@ constexpr int MAX_EVENTS = 4 * 2048;
 constexpr u64 TK_STAGE_MAX_FRAC = 16;  // staged top-k (k_main<5/6>) for k <= n / 16
 constexpr int TK5_SPLIT = 4;            // workgroups per k_main workgroup in k_tk5_count / k_tk5_write (window-parallel)
 constexpr int COOP_BACKOFF = 64;        // synchronous selects on the per-level path after a grid-barrier timeout
+constexpr uint64_t DSCAN_PER_WG = 1ull << 15;  // candidates per workgroup of the sharded scan's first-digit histogram
 
 #define HIP_TRY(x)                                                                                    \
     do {                                                                                              \
@@ -89,6 +90,7 @@ struct kth_ctx {
     int main_grid[7] = {0, 0, 0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
     bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
     bool fault_barrier = false;    // KTH_FAULT_BARRIER (tests): k_finish reports a grid-barrier timeout
+    bool fault_once = false;       // KTH_FAULT_BARRIER=once: only the first cooperative launch does
     bool topk_stage = true;        // staged top-k (k_main<5/6>); KTH_TOPK_STAGE=0 turns it off
     u64 topk_seg_cap = 0;          // KTH_TOPK_SEG_CAP (tests): entries per staging segment (0 = sized from n)
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
@@ -145,7 +147,14 @@ struct kth_ctx {
     // sharded protocol
     u64 *uslots = nullptr;
     int64_t dist_n = 0, dist_k = 0, dist_cap = 0;
-    int dist_level_next = 0;
+    int dist_level_next = 0;   // the next kth_dist_level call's level (-1: none expected)
+    u64 dscan_per_wg = DSCAN_PER_WG;  // k_dscan_hist keys per workgroup (KTH_DSCAN_PER_WG)
+    int dist_levels = -1;      // level calls that return a slot (from level 0's DistStatus; -1: unknown yet)
+    int dist_result_slot = -1; // the slot the last level accumulated into (kth_dist_result reads it)
+    uint32_t *h_dist = nullptr;  // DistStatus, host-visible (pinned, mapped), written by level 0's k_dlevel
+    uint32_t *d_dist = nullptr;  // ... its device address
+    hipEvent_t ev_dist = nullptr;  // recorded after level 0
+    uint32_t dist_tag = 0;     // level 0 calls so far (the DistStatus tag)
 };
 
 namespace {
@@ -358,6 +367,7 @@ kth::CoopArgs coop_args(kth_ctx *c, u64 slot_off, int32_t *d_out, int32_t *d_sta
     x.sparse_per_wg = FIN_SPARSE_PER_WG;
     x.slack64 = c->head_slack64;
     x.fault = c->fault_barrier ? 1u : 0u;
+    if (c->fault_once) c->fault_barrier = false;
     return x;
 }
 
@@ -512,10 +522,18 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
     return launch_check();
 }
 
+// After a grid-barrier timeout the cooperative kernels stay off for
+// COOP_BACKOFF selections of any entry point (synchronous, asynchronous,
+// top-k, sharded); each one counts down here, then they are tried again.
+void coop_tick(kth_ctx *c) {
+    if (c->coop_backoff > 0 && --c->coop_backoff == 0) c->coop = c->coop_wanted;
+}
+
 int select_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int32_t *d_out, int32_t *d_status,
                  int tflag = 0, uint32_t *tflags = nullptr) {
     if (!c || !d_keys || (!d_out && !d_status) || n < 1 || k < 1 || k > n) return KTH_EINVAL;
     KTH_TRY(set_device(c));
+    coop_tick(c);
     if (c->dirty) {
         HIP_TRY(hipMemsetAsync(c->islots, 0, SLOT_ALLOC_WORDS * sizeof(u64), c->stream));
         c->dirty = false;
@@ -674,6 +692,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
                 c->main_grid[v] = c->num_cu * per;
             }
             if (const char *g = getenv("KTH_SPARSE_PER_WG")) c->sparse_per_wg = (u64)std::max(0, atoi(g));
+            if (const char *g = getenv("KTH_DSCAN_PER_WG")) c->dscan_per_wg = (u64)std::max(1024, atoi(g));
             if (const char *g = getenv("KTH_POST_DENSE_GRID")) c->post_dense_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_COOP")) c->coop = atoi(g) != 0;
@@ -683,7 +702,10 @@ int kth_ctx_create(int device, kth_ctx **out) {
             // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
             // so its count pass must report the bracket failure
             c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
-            c->fault_barrier = getenv("KTH_FAULT_BARRIER") != nullptr;
+            if (const char *g = getenv("KTH_FAULT_BARRIER")) {
+                c->fault_barrier = true;
+                c->fault_once = !strcmp(g, "once");
+            }
             if (const char *g = getenv("KTH_TOPK_STAGE")) c->topk_stage = atoi(g) != 0;
             if (const char *g = getenv("KTH_TOPK_SEG_CAP")) c->topk_seg_cap = (u64)std::max(0, atoi(g));
         }
@@ -771,6 +793,8 @@ int kth_ctx_destroy(kth_ctx *c) {
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->h_status) (void)hipHostFree(c->h_status);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_dist) (void)hipHostFree(c->h_dist);
+    if (c->ev_dist) (void)hipEventDestroy(c->ev_dist);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     if (tl_ctx == c) tl_ctx = nullptr;
     delete c;
@@ -817,7 +841,6 @@ int kth_select_i32_async(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k
 int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *out) {
     if (!c || !keys || !out || n < 1 || k < 1 || k > n) return KTH_EINVAL;
     KTH_TRY(set_device(c));
-    if (c->coop_backoff > 0 && --c->coop_backoff == 0) c->coop = c->coop_wanted;  // try the grid barriers again
     const int32_t *dk = keys;
     if (!is_device_ptr(keys)) {
         KTH_TRY(grow(reinterpret_cast<void **>(&c->staging), &c->staging_cap, (u64)n * 4));
@@ -835,7 +858,7 @@ int kth_select_i32_ctx(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, in
         // contended, every cooperative launch would spin out its barriers)
         c->dirty = true;
         c->coop = false;
-        c->coop_backoff = COOP_BACKOFF;
+        c->coop_backoff = COOP_BACKOFF + 1;  // (the retry below counts one)
         KTH_TRY(select_async(c, dk, n, k, nullptr, c->d_status));
         HIP_TRY(hipMemcpyAsync(c->h_status, c->d_status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
@@ -860,6 +883,11 @@ int kth_select_i32(const int32_t *keys, int64_t n, int64_t k, int32_t *out) {
         KTH_TRY(kth_ctx_create(dev, &tl_ctx));
     }
     return kth_select_i32_ctx(tl_ctx, keys, n, k, out);
+}
+
+int kth_ctx_coop(const kth_ctx *c) {
+    if (!c) return KTH_EINVAL;
+    return c->coop ? 1 : 0;
 }
 
 int kth_ctx_last_stats(kth_ctx *c, kth_stats *out) {
@@ -1142,10 +1170,23 @@ int kth_window_slack64(void) { return (int)(HEAD_SLACK * 64); }
 int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     if (!c || !d_slots || n_total < 1 || k < 1 || k > n_total) return KTH_EINVAL;
     KTH_TRY(set_device(c));
+    if (!c->h_dist) {  // level 0's DistStatus: host-visible memory the kernel writes, an event after it
+        if (hipHostMalloc(reinterpret_cast<void **>(&c->h_dist), kth::DIST_STATUS_WORDS * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            c->h_dist = nullptr;
+            return KTH_ENOMEM;
+        }
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_dist), c->h_dist, 0));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_dist, hipEventDisableTiming));
+    }
+    coop_tick(c);
     c->uslots = reinterpret_cast<u64 *>(d_slots);
     c->dist_n = n_total;
     c->dist_k = k;
-    c->dist_level_next = 0;
+    c->dist_level_next = -1;  // kth_dist_scan first
+    c->dist_levels = -1;
+    c->dist_result_slot = -1;
     c->dist_zero = true;  // kth_dist_sample clears the slots inside its kernel
     // the ctx's own slots are left zeroed by every completed k_result; a
     // sequence cut short (dirty, or a dist selection never finished) re-zeroes,
@@ -1233,32 +1274,67 @@ int kth_dist_scan(kth_ctx *c, const int32_t *d_keys, int64_t n_local) {
     if (!c || !d_keys || n_local < 0 || !c->uslots) return KTH_EINVAL;
     KTH_TRY(set_device(c));
     KTH_TRY(reserve_cand(c, std::max<int64_t>(n_local, 1)));
-    StepArgs a = c->dist_coop_window ? step(c, kth::ADV_CARRY, 0, 1, nullptr, c->uslots, nullptr)
-                                     : step(c, kth::ADV_PICK, 0, 1, islot(c, 0), c->uslots, nullptr);
+    u64 *U0 = c->uslots;
+    StepArgs a = c->dist_coop_window ? step(c, kth::ADV_CARRY, 0, 1, nullptr, U0, nullptr)
+                                     : step(c, kth::ADV_PICK, 0, 1, islot(c, 0), U0, nullptr);
     a.keys = d_keys;
     a.n_local = (u64)n_local;
     ev_main(c);
     kth::k_main<0><<<c->main_grid[0], kth::BLK, 0, c->stream>>>(a, c->cand, nullptr, nullptr, kth::TkSeg{});
     ev_main(c);
-    c->dist_level_next = 0;
     KTH_TRY(launch_check());
+    // this rank's candidates' first digit into the same slot (one all-reduce
+    // carries the counts and the digit)
+    a = step(c, kth::ADV_CARRY, 1, 1, nullptr, U0, nullptr);
+    a.min_per_wg = c->dscan_per_wg;
+    kth::k_dscan_hist<kth::DENSE_BLK><<<level_grid(cand_capacity(std::max<int64_t>(n_local, 1)), c->dscan_per_wg),
+                                        kth::DENSE_BLK, 0, c->stream>>>(a);
+    KTH_TRY(launch_check());
+    c->dist_level_next = 0;
+    c->dist_levels = -1;
     return 0;
 }
 
+// Level l reads state l+1 (mod 2) and slot l (mod 3), writes state l (mod 2),
+// accumulates into slot l+1 and clears slot l+2; level 0 also tells the host
+// (DistStatus) how many level calls return a slot, so that level 1 can answer
+// KTH_DIST_DONE without a collective.  Level 0 is enqueued without waiting
+// for anything; level 1 waits for level 0 (the host reads the DistStatus) --
+// while the all-reduce after level 0 is still queued on the device.
 int kth_dist_level(kth_ctx *c, const int32_t *d_keys, int64_t n_local, int level) {
-    if (!c || !d_keys || n_local < 0 || !c->uslots || level < 0 || level >= KTH_DIST_LEVELS ||
-        level != c->dist_level_next)
-        return KTH_EINVAL;
+    if (!c || !d_keys || n_local < 0 || !c->uslots || level < 0 || level != c->dist_level_next) return KTH_EINVAL;
     KTH_TRY(set_device(c));
+    if (level >= 1 && c->dist_levels < 0) {
+        HIP_TRY(hipEventSynchronize(c->ev_dist));
+        const uint32_t *h = c->h_dist;
+        const uint32_t levels = __atomic_load_n(&h[0], __ATOMIC_ACQUIRE), tag = __atomic_load_n(&h[3], __ATOMIC_ACQUIRE);
+        if (tag != c->dist_tag || levels < 1 || levels > KTH_DIST_MAX_LEVELS) {
+            c->dirty = true;
+            return KTH_EINTERNAL;
+        }
+        c->dist_levels = (int)levels;
+    }
+    if (level >= 1 && level >= c->dist_levels) {
+        c->dist_result_slot = level % 3;  // accumulated by level - 1
+        c->dist_level_next = -1;
+        return KTH_DIST_DONE;
+    }
     u64 *U[3] = {c->uslots, c->uslots + KTH_STATS_WORDS, c->uslots + 2 * KTH_STATS_WORDS};
     const int in = level % 3, acc = (level + 1) % 3, zero = (level + 2) % 3;
-    // states: scan wrote st[1]; level l reads st[(l+1)%2] and writes st[l%2]
     StepArgs a = step(c, level == 0 ? kth::ADV_DECIDE : kth::ADV_PICK, (level + 1) % 2, level % 2, U[in], U[acc],
-                      level == 0 ? nullptr : U[zero]);
+                      U[zero]);
     a.keys = d_keys;
     a.n_local = (u64)n_local;
-    launch_level(c, a, level == 0, LEVEL_GRID_MAX);
+    a.min_per_wg = sparse_wg(c);     // a digit under a resolved prefix: only that bin's keys
+    a.dense_per_wg = DENSE_PER_WG;   // the fallback's first digit over the whole shard
+    if (level == 0) {
+        a.host_status = c->d_dist;
+        a.tag = ++c->dist_tag;
+    }
+    // (the active workgroups follow the domain's size: candidates or the shard)
+    kth::k_dlevel<kth::BLK><<<LEVEL_GRID_MAX, kth::BLK, 0, c->stream>>>(a);
     KTH_TRY(launch_check());
+    if (level == 0) HIP_TRY(hipEventRecord(c->ev_dist, c->stream));
     c->dist_level_next = level + 1;
     return acc;
 }
@@ -1276,16 +1352,51 @@ int kth_internal_slots_sum(uint64_t *const *slots, int P, int slot, void *stream
     return launch_check();
 }
 
+int kth_internal_status_gather(kth_ctx *const *ctxs, int P, int32_t *d_dst, void *stream) {
+    if (!ctxs || !d_dst || P < 1 || P > KTH_LOCAL_MAX_SHARDS) return KTH_EINVAL;
+    kth::StatusPtrs p{};
+    for (int i = 0; i < P; ++i) {
+        if (!ctxs[i] || ctxs[i]->device != ctxs[0]->device) return KTH_EINVAL;
+        p.p[i] = ctxs[i]->d_status;
+    }
+    KTH_TRY(set_device(ctxs[0]));
+    kth::k_status_gather<<<1, kth::WAVE, 0, reinterpret_cast<hipStream_t>(stream)>>>(p, P, d_dst);
+    return launch_check();
+}
+
+int kth_internal_dist_window_share(kth_ctx *src, kth_ctx *const *dst, int P) {
+    if (!src || !dst || P < 0 || P > KTH_LOCAL_MAX_SHARDS) return KTH_EINVAL;
+    if (!src->dist_coop_window) return 1;  // per-level window: its last pick is the scan's, nothing to copy
+    kth::StatePtrs d{};
+    for (int i = 0; i < P; ++i) {
+        if (!dst[i] || dst[i]->device != src->device || !dst[i]->uslots) return KTH_EINVAL;
+        d.p[i] = dst[i]->st;  // (the window's state is st[0], kth_dist_scan carries it)
+    }
+    if (P == 0) return KTH_OK;
+    KTH_TRY(set_device(src));
+    kth::k_state_bcast<<<1, kth::BLK, 0, src->stream>>>(src->st, d, P);
+    KTH_TRY(launch_check());
+    for (int i = 0; i < P; ++i) {
+        dst[i]->dist_coop_window = true;
+        dst[i]->dist_zero = false;
+    }
+    return KTH_OK;
+}
+
 int kth_dist_result(kth_ctx *c, int32_t *d_out) {
-    if (!c || !d_out || !c->uslots || c->dist_level_next != KTH_DIST_LEVELS) return KTH_EINVAL;
+    if (!c || !d_out || !c->uslots || c->dist_result_slot < 0) return KTH_EINVAL;
     KTH_TRY(set_device(c));
-    const int in = KTH_DIST_LEVELS % 3;  // slot written by the last level
-    const int st_in = (KTH_DIST_LEVELS - 1) % 2;
-    StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)in * KTH_STATS_WORDS, nullptr, nullptr);
+    const int L = c->dist_levels;  // levels enqueued: the last wrote state (L - 1) % 2
+    const int st_in = (L + 1) % 2;
+    StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)c->dist_result_slot * KTH_STATS_WORDS,
+                      nullptr, nullptr);
     // (the islots and, right after them, k_head's slots of a cooperative window)
-    kth::k_result<<<1, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots, ISLOT_WORDS + HSLOT_WORDS);
+    static_assert(ISLOT_WORDS % 2 == 0, "k_dresult zeroes 16-byte words from the islots on");
+    kth::k_dresult<kth::BLK><<<16, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots,
+                                                            ISLOT_WORDS + HSLOT_WORDS);
     c->last_state = 1 - st_in;
     c->dist_level_next = -1;
+    c->dist_result_slot = -1;
     c->dist_open = false;
     return launch_check();
 }

@@ -59,8 +59,9 @@ struct alignas(16) SelState {
     Target t[2];
     uint32_t mode, W, base, lo, hi, answer, error, path;
     uint32_t share;    // target 1 reads target 0's histogram this level
-    uint32_t d0;       // width of a domain's first digit (0: DIGIT); later digits are DIGIT wide
-    uint32_t pad[2];
+    uint32_t d0;       // width of a domain's first digit (0: DIGIT)
+    uint32_t dw;       // width of its later digits (0: DIGIT; the sharded protocol's digits: DDIG)
+    uint32_t pad;
     u64 below, eqv;    // done: keys below the answer, keys equal to it (0 = unknown); kth_topk_i32
 };
 
@@ -81,9 +82,10 @@ __device__ __forceinline__ uint32_t digit_bits(uint32_t W, uint32_t done) {
     uint32_t r = W - done;
     return r < (uint32_t)DIGIT ? r : (uint32_t)DIGIT;
 }
-// the next digit of a selection state: the first one may be narrower (d0)
+// the next digit of a selection state: the first one may be narrower (d0),
+// the later ones are dw wide (DIGIT unless set)
 __device__ __forceinline__ uint32_t digit_bits(const SelState &s, uint32_t done) {
-    const uint32_t r = s.W - done, d = (done == 0 && s.d0) ? s.d0 : (uint32_t)DIGIT;
+    const uint32_t r = s.W - done, d = (done == 0 && s.d0) ? s.d0 : (s.dw ? s.dw : (uint32_t)DIGIT);
     return r < d ? r : d;
 }
 

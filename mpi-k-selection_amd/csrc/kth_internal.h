@@ -22,6 +22,21 @@ extern "C" {
 __attribute__((visibility("hidden"))) int kth_internal_slots_sum(uint64_t *const *slots, int P, int slot,
                                                                  void *stream);
 
+/* The local transport's window: after kth_dist_window(src), the window state
+ * copied to every dst[i] (ctxs of the same device, each bound by
+ * kth_dist_begin and sampled), enqueued on src's stream, as if each had run
+ * kth_dist_window on the same gathered sample.  Returns 1 (nothing done; run
+ * kth_dist_window on each) when src's window was not a cooperative one. */
+struct kth_ctx;
+__attribute__((visibility("hidden"))) int kth_internal_dist_window_share(struct kth_ctx *src,
+                                                                         struct kth_ctx *const *dst, int P);
+
+/* Every ctxs[i]'s last [answer, error] words (k_dresult's d_status) to
+ * d_dst[2 i], d_dst[2 i + 1] (device-visible host memory), enqueued on
+ * `stream`; ctxs of one device. */
+__attribute__((visibility("hidden"))) int kth_internal_status_gather(struct kth_ctx *const *ctxs, int P,
+                                                                     int32_t *d_dst, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

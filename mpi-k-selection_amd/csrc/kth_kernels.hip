@@ -71,6 +71,9 @@ struct StepArgs {
     u64 min_per_wg;        // keys per active workgroup (sets how many WGs flush a histogram)
     u64 *stamps;           // KTH_STAMPS diagnostics: [gridDim.x][8] wall-clock stamps, else null
     u64 zero_words;        // k_gather<false> (sharded sample): clear stats_zero[0 .. zero_words)
+    uint32_t *host_status; // k_dlevel, level 0 of the sharded protocol: DistStatus in host-visible memory
+    uint32_t tag;          // ... with this tag (the host's call counter)
+    u64 dense_per_wg;      // k_dlevel: keys per active workgroup for a domain's first digit
 };
 
 // Diagnostic phase stamps (KTH_STAMPS=1 only; null pointer in the product):
@@ -1294,6 +1297,279 @@ __global__ __launch_bounds__(BLK) void k_result(StepArgs a, int32_t *d_out, int3
     KTH_STAMP(a, 5);
 }
 
+// ------------------------------------------------ sharded protocol (kth_dist_*)
+// One all-gather (the samples) and, in the common case, two all-reduces per
+// selection (TODO-kth-problem-cgm.c:122-233 runs 2 gathers, a broadcast and an
+// all-reduce per round, ~12 rounds):
+//   kth_dist_scan   k_main<0> (counts) + k_dscan_hist: this rank's candidates'
+//                   FIRST digit into the same slot             -> all-reduce 1
+//   level 0         k_dlevel: decide from the reduced counts, pick the first
+//                   candidate digit from the same slot, histogram the next
+//                                                                -> all-reduce 2
+//   result          k_dresult: pick the last digit
+// The candidate domain's digits are taken relative to lo + 1 and are DDIG = 12
+// bits wide (one target: a slot's two 2048-word histograms hold one 4096-bin
+// digit), the narrow one first, so a window of width <= 2^24 needs exactly
+// these two.  Wider windows and the exact fallback over the whole shard (a
+// window miss or a candidate overflow: 8 + 12 + 12 bits) take more levels;
+// level 0 tells the host how many (DistStatus), so every rank makes the same
+// calls.
+constexpr int DDIG = 12;
+constexpr int DNB = 1 << DDIG;
+static_assert(DNB == 2 * NBINS, "a stats slot's histogram words hold one DDIG-bit digit");
+constexpr uint32_t DIST_FULL_D0 = 32 - 2 * DDIG;  // the fallback's first digit (8 bits)
+
+// The candidate domain of a window [lo, hi]: keys lo < x < hi, as x - base in
+// [0, 2^W) with base = lo + 1; d0 = first digit width (the later ones DDIG).
+struct CandDom {
+    uint32_t base, W, d0;
+};
+__device__ __forceinline__ CandDom cand_domain(uint32_t lo, uint32_t hi) {
+    CandDom d{lo + 1u, 0u, 0u};
+    if (hi - lo < 2u) return d;  // no key strictly inside
+    const uint32_t range = hi - lo - 2u;
+    d.W = range ? 32u - (uint32_t)__clz(range) : 0u;
+    const uint32_t nd = (d.W + DDIG - 1) / DDIG;
+    d.d0 = d.W - (uint32_t)DDIG * (nd ? nd - 1u : 0u);
+    return d;
+}
+
+// decide() for the sharded protocol: the same rule, the DDIG-bit digits
+__device__ __forceinline__ void decide_dist(SelState &s, const u64 *c) {
+    const u64 L = c[C_LT], E1 = c[C_EQLO], M = c[C_IN], ovf = c[C_OVF];
+    const u64 E2 = (s.lo == s.hi) ? 0 : c[C_EQHI];
+    for (int i = 0; i < 5; ++i) s.cnt[i] = c[i];
+    const u64 k = s.k;
+    s.t[1].active = 0;
+    s.t[0] = Target{k, 0, 0, 1, 0};
+    s.path = 3;  // KTH_PATH_WINDOW
+    s.dw = DDIG;
+    if (k > L && k <= L + E1) {
+        s.answer = s.lo;
+        s.mode = MODE_DONE;
+    } else if (k > L + E1 && k <= L + E1 + M && ovf == 0) {
+        const CandDom d = cand_domain(s.lo, s.hi);
+        s.base = d.base;
+        s.W = d.W;
+        s.d0 = d.d0;
+        s.t[0].k = k - L - E1;
+        s.mode = MODE_CAND;
+        if (s.W == 0) {
+            s.answer = s.base;
+            s.mode = MODE_DONE;
+        }
+    } else if (k > L + E1 + M && k <= L + E1 + M + E2) {
+        s.answer = s.hi;
+        s.mode = MODE_DONE;
+    } else {
+        s.mode = MODE_FULL;
+        s.W = 32;
+        s.base = 0;
+        s.d0 = DIST_FULL_D0;
+        s.path = 4;  // KTH_PATH_WINDOW_FALLBACK
+    }
+}
+
+__device__ __forceinline__ bool dist_live(const SelState &s) {
+    return (s.mode == MODE_CAND || s.mode == MODE_FULL) && s.t[0].done < s.W;
+}
+
+// The pick of one DDIG-bit digit: thread i holds bins [i*PER, i*PER + PER).
+template <int BLOCK>
+__device__ __forceinline__ void pick_wide(SelState &ss, const u64 (&h)[DNB / BLOCK], u64 *scratch) {
+    if (!dist_live(ss)) return;  // block-uniform (ss in LDS after a barrier)
+    uint32_t bin;
+    u64 below;
+    const bool ok = block_pick_vals<BLOCK, DNB / BLOCK>(h, ss.t[0].k, &bin, &below, scratch);
+    if (threadIdx.x == 0) {
+        const uint32_t d = digit_bits(ss, ss.t[0].done);
+        if (!ok || bin >= (1u << d)) {
+            ss.error = 1;
+            ss.mode = MODE_DONE;
+        } else {
+            ss.t[0].k -= below;
+            ss.t[0].prefix = (ss.t[0].prefix << d) | bin;
+            ss.t[0].done += d;
+            resolve(ss);
+        }
+    }
+    __syncthreads();
+}
+
+// The state of the previous step (a.st_in) into LDS; ADV_DECIDE (level 0):
+// the decide from a.stats_in's reduced counts.  Everything a workgroup needs
+// to know whether it has work (the domain and its size) comes from this
+// alone, so idle workgroups leave before loading a histogram.
+template <int BLOCK>
+__device__ __forceinline__ void dist_state(SelState &ss, const StepArgs &a, u64 *cnts) {
+    constexpr int SV = sizeof(SelState) / 16;
+    static_assert(SV <= BLOCK && NCOUNTS <= BLOCK, "state and counts load in one step");
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x < SV) sv = reinterpret_cast<const uint4 *>(a.st_in)[threadIdx.x];
+    if (a.adv == ADV_DECIDE && threadIdx.x < NCOUNTS) cnts[threadIdx.x] = a.stats_in[threadIdx.x];
+    if (threadIdx.x < SV) reinterpret_cast<uint4 *>(&ss)[threadIdx.x] = sv;
+    __syncthreads();
+    if (a.adv == ADV_DECIDE) {
+        if (threadIdx.x == 0 && ss.mode == MODE_MAIN) decide_dist(ss, cnts);
+        __syncthreads();
+    }
+}
+
+// The digit pick of a step: level 0 picks the candidates' first digit (the
+// scan's slot holds it; the fallback has none yet), later steps the digit
+// the previous level histogrammed.
+template <int BLOCK>
+__device__ __forceinline__ void dist_pick(SelState &ss, const StepArgs &a, u64 *scratch) {
+    if (a.adv == ADV_DECIDE ? ss.mode != MODE_CAND : !dist_live(ss)) return;  // block-uniform
+    constexpr int PER = DNB / BLOCK;
+    const u64 *b = a.stats_in + NCOUNTS + threadIdx.x * PER;
+    u64 h[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) h[j] = b[j];
+    pick_wide<BLOCK>(ss, h, scratch);
+}
+
+// Histogram digit `d` (bits [W - done - d, W - done) of key - base) of the keys
+// of `dom` whose resolved prefix matches, into LDS, and flush it to acc's
+// histogram words.  XOR: the domain is the raw int32 shard.
+template <int BLOCK, bool XOR>
+__device__ __forceinline__ void dist_hist(uint32_t *lh, const uint32_t *dom, u64 count, uint32_t active,
+                                          uint32_t base, uint32_t W, uint32_t done, uint32_t prefix, uint32_t d,
+                                          u64 *acc) {
+    const uint32_t sh = W - done - d, mask = (1u << d) - 1u, msh = W - done;
+    auto f = [&](const uint32_t *k, uint32_t valid, auto full) {
+#pragma unroll
+        for (int j = 0; j < 4 * LEVEL_UNROLL; ++j) {
+            const uint32_t v = k[j] - base;
+            // (a 64-bit shift: msh is 32 before the first digit)
+            if ((decltype(full)::value || ((valid >> j) & 1u)) && ((u64)v >> msh) == (u64)prefix)
+                atomicAdd(&lh[(v >> sh) & mask], 1u);
+        }
+    };
+    if (blockIdx.x < active) stream_tiles<BLOCK, LEVEL_UNROLL, XOR>(dom, count, blockIdx.x, active, f);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b <= mask; b += BLOCK) {
+        const uint32_t c = lh[b];
+        if (c) atomicAdd(&acc[NCOUNTS + b], (u64)c);
+    }
+}
+
+// What level 0 tells the host (written to host-visible memory by workgroup 0):
+// how many kth_dist_level calls return a slot to all-reduce (level 0's
+// included), so that every rank stops at the same call; the mode and W after
+// level 0's pick; the host's tag of the call.
+struct DistStatus {
+    uint32_t levels, mode, W, tag;
+};
+constexpr int DIST_STATUS_WORDS = sizeof(DistStatus) / 4;
+
+// kth_dist_scan's second kernel: this rank's candidates' first digit (the
+// domain of cand_domain(lo, hi)) into the count slot a.stats_acc.  The window
+// is in a.st_in (k_main's state).  Nothing to do when the window holds no key
+// strictly inside or one value (W = 0: decide needs no digit).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_dscan_hist(StepArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lh[DNB];
+    const SelState *st = a.st_in;
+    const uint32_t mode = st->mode, lo = st->lo, hi = st->hi;
+    const u64 count = min(*a.cand_count, a.cap);
+    if (mode != MODE_MAIN) return;
+    const CandDom dm = cand_domain(lo, hi);
+    if (dm.W == 0 || count == 0) return;
+    const uint32_t active = (uint32_t)min((u64)gridDim.x, (count + a.min_per_wg - 1) / a.min_per_wg);
+    if (blockIdx.x >= active) return;
+    for (int i = threadIdx.x; i < DNB / 4; i += BLOCK) reinterpret_cast<uint4 *>(lh)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    dist_hist<BLOCK, false>(lh, a.cand, count, active, dm.base, dm.W, 0u, 0u, dm.d0, a.stats_acc);
+}
+
+// One level of the sharded protocol: the state (and at level 0 the decide),
+// the pick, then the next digit's histogram over the candidates (MODE_CAND)
+// or the shard (MODE_FULL): keys per workgroup a.min_per_wg for a digit under
+// a resolved prefix (sparse), a.dense_per_wg for a domain's first digit (every
+// key lands: the fallback's level 0).  Workgroup 0 publishes the state,
+// clears the slot the next level accumulates into and (level 0) writes the
+// DistStatus.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_dlevel(StepArgs a) {
+    __shared__ SelState ss;
+    __shared__ u64 scratch[2 * (BLOCK / WAVE) + 8];
+    __shared__ u64 cnts[NCOUNTS];
+    __shared__ __attribute__((aligned(16))) uint32_t lh[DNB];
+    const u64 cand_n = min(*a.cand_count, a.cap);
+    dist_state<BLOCK>(ss, a, cnts);
+    {  // workgroups without keys to histogram leave before the pick's loads
+        const uint32_t m = ss.mode;
+        // the digit after the pick is a domain's first only for the fallback's
+        // level 0 (no pick there); a live state otherwise picks one first
+        const bool first = a.adv == ADV_DECIDE && m == MODE_FULL;
+        const u64 count = m == MODE_CAND ? cand_n : m == MODE_FULL ? a.n_local : 0;
+        const u64 per = first ? a.dense_per_wg : a.min_per_wg;
+        if (blockIdx.x != 0 && (u64)blockIdx.x * per >= count) return;  // block-uniform
+    }
+    for (int i = threadIdx.x; i < DNB / 4; i += BLOCK) reinterpret_cast<uint4 *>(lh)[i] = make_uint4(0, 0, 0, 0);
+    dist_pick<BLOCK>(ss, a, scratch);
+    __syncthreads();
+    const bool live = dist_live(ss);
+    const uint32_t mode = ss.mode, W = ss.W, done = ss.t[0].done, prefix = ss.t[0].prefix, base = ss.base;
+    const uint32_t d = live ? digit_bits(ss, done) : 0u;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            *a.st_out = ss;
+            if (a.host_status) {
+                // this level's slot, then one per DDIG bits left after its digit
+                const uint32_t left = live ? W - done - d : 0u;
+                const uint32_t v[DIST_STATUS_WORDS] = {1u + (left + DDIG - 1) / DDIG, mode, W, a.tag};
+#pragma unroll
+                for (int i = 0; i < DIST_STATUS_WORDS; ++i)
+                    __hip_atomic_store(&a.host_status[i], v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        if (a.stats_zero)
+            for (int i = threadIdx.x; i < STATS_WORDS; i += BLOCK) a.stats_zero[i] = 0;
+    }
+    if (!live) return;  // block-uniform
+    const u64 count = mode == MODE_CAND ? cand_n : a.n_local;
+    const u64 per = done == 0 ? a.dense_per_wg : a.min_per_wg;
+    const uint32_t active = (uint32_t)min((u64)gridDim.x, (count + per - 1) / per);
+    if (blockIdx.x >= active) return;
+    if (mode == MODE_FULL)
+        dist_hist<BLOCK, true>(lh, reinterpret_cast<const uint32_t *>(a.keys), count, active, base, W, done, prefix,
+                               d, a.stats_acc);
+    else
+        dist_hist<BLOCK, false>(lh, a.cand, count, active, base, W, done, prefix, d, a.stats_acc);
+}
+
+// The sharded protocol's last step: workgroup 0 picks the last digit and
+// writes the answer (only a verified one reaches d_out); every workgroup
+// zeroes its share of the ctx-internal slots (16-byte stores).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_dresult(StepArgs a, int32_t *d_out, int32_t *d_status, u64 *izero,
+                                                   u64 izero_words) {
+    __shared__ SelState ss;
+    __shared__ u64 scratch[2 * (BLOCK / WAVE) + 8];
+    __shared__ u64 cnts[NCOUNTS];
+    if (blockIdx.x == 0) {
+        dist_state<BLOCK>(ss, a, cnts);
+        dist_pick<BLOCK>(ss, a, scratch);
+        if (threadIdx.x == 0) {
+            SelState o = ss;
+            if (o.mode != MODE_DONE && !o.error) o.error = 16 + o.mode;
+            *a.st_out = o;
+            if (d_out && !o.error) *d_out = i32_of_key(o.answer);
+            if (d_status) {
+                d_status[0] = i32_of_key(o.answer);
+                d_status[1] = (int32_t)o.error;
+            }
+        }
+    }
+    // (izero is 16-byte aligned; an odd word count leaves one u64)
+    uint4 *z = reinterpret_cast<uint4 *>(izero);
+    const u64 nz = izero_words / 2;
+    for (u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x; i < nz; i += (u64)gridDim.x * BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+    if ((izero_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) izero[izero_words - 1] = 0;
+}
+
 // n <= 16384: whole selection in one workgroup, keys in LDS.
 __global__ __launch_bounds__(SMALL_BLOCK) void k_small(const int32_t *__restrict__ keys, u64 n, u64 k,
                                                        int32_t *d_out, int32_t *d_status, SelState *st_out) {
@@ -1438,6 +1714,29 @@ __global__ __launch_bounds__(BLK) void k_slots_sum(SlotPtrs s, int P, u64 words)
         for (int r = 0; r < P; ++r) sum += s.p[r][i];
         for (int r = 0; r < P; ++r) s.p[r][i] = sum;
     }
+}
+
+// The sharded handle's final read-back: every shard's [answer, error] words
+// (the ctx's d_status, written by k_dresult) into one host-visible array, so
+// one synchronisation reads them all.
+struct StatusPtrs {
+    const int32_t *p[SLOTS_SUM_MAX];
+};
+__global__ __launch_bounds__(WAVE) void k_status_gather(StatusPtrs src, int P, int32_t *dst) {
+    for (int i = threadIdx.x; i < 2 * P; i += WAVE)
+        __hip_atomic_store(&dst[i], src.p[i / 2][i % 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The local transport's window: every shard derives the same window from the
+// same gathered sample, so on one device it is computed once (k_head on
+// shard 0's ctx) and its state copied to the other shards' ctxs.
+struct StatePtrs {
+    SelState *p[SLOTS_SUM_MAX];
+};
+__global__ __launch_bounds__(BLK) void k_state_bcast(const SelState *src, StatePtrs dst, int P) {
+    constexpr int SV = sizeof(SelState) / 16;
+    for (int i = threadIdx.x; i < SV * P; i += BLK)
+        reinterpret_cast<uint4 *>(dst.p[i / SV])[i % SV] = reinterpret_cast<const uint4 *>(src)[i % SV];
 }
 
 }  // namespace kth

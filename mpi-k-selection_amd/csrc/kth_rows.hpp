@@ -548,6 +548,9 @@ template <bool F32, int KPL, int R0, bool KEYS_OUT, bool STAGE = false>
 __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
                                                     uint32_t flip, uint32_t *eq_out = nullptr,
                                                     const TopkOut *tko = nullptr, bool *topk_done = nullptr) {
+    // a dense bin's radix fallback (row_select_dense_bin) counts into 4 copies
+    // of the wave's histogram: the caller sizes it R0 * RW_STRIDE words
+    static_assert(R0 >= 4, "row_select_dense_bin needs at least 4 histogram copies per wave");
     auto to_keys = [&]() {
 #pragma unroll
         for (int j = 0; j < KPL; ++j) {

@@ -10,12 +10,14 @@
 //
 //   per device: begin, sample           -> ncclAllGather of the samples
 //   per device: window, scan            -> ncclAllReduce of the counts slot
-//   per device: level l (3 levels)      -> ncclAllReduce of the histogram slot
+//                                          (+ the candidates' first digit)
+//   per device: level l (usually one)   -> ncclAllReduce of the histogram slot
 //   per device: result                  -> every device holds the same answer
 //
 // Each device's work is enqueued on its own ctx stream, the collectives on the
-// same streams, so the host never waits between steps; it synchronises once at
-// the end to read the answer.  RCCL is resolved at first use (dlopen of the
+// same streams; the host waits once before the second level call (for level
+// 0's DistStatus: how many levels follow, while the device still has the
+// all-reduce after level 0 queued) and once at the end to read the answer.  RCCL is resolved at first use (dlopen of the
 // librccl.so.1 already in the process, e.g. torch's, or the system one), so
 // libkth.so itself does not depend on it.
 //
@@ -136,6 +138,8 @@ struct kth_sharded {
     bool local = false;           // every shard on one device: the local transport (no RCCL)
     uint32_t *lgathered = nullptr;  // local transport: the gathered sample (every shard's at its offset)
     int64_t lgathered_cap = 0;
+    int32_t *h_status = nullptr;  // per shard [answer, error], host-visible (pinned, mapped, portable)
+    int32_t *d_status = nullptr;  // ... its device address
     double enqueue_us = 0;  // host time of the last select up to its last enqueue (kth_sharded_enqueue_us)
 };
 
@@ -188,6 +192,7 @@ int kth_sharded_destroy(kth_sharded *h) {
         (void)hipSetDevice(h->d[0].device);
         (void)hipFree(h->lgathered);
     }
+    if (h->h_status) (void)hipHostFree(h->h_status);
     delete h;
     return KTH_OK;
 }
@@ -237,6 +242,13 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
             rc = KTH_ENOMEM;
             break;
         }
+    }
+    if (rc == KTH_OK) {  // the answers' read-back buffer
+        if (hipSetDevice(devices[0]) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&h->h_status), 2 * (size_t)ngpu * sizeof(int32_t),
+                          hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&h->d_status), h->h_status, 0) != hipSuccess)
+            rc = KTH_ENOMEM;
     }
     if (rc == KTH_OK && !local) {
         if (rccl().CommInitAll(comms.data(), ngpu, devices) != ncclSuccess)
@@ -303,7 +315,6 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
         s_off[(size_t)i + 1] = s_off[(size_t)i] + s_dev[(size_t)i];
         equal = equal && s_dev[(size_t)i] == s_dev[0];
     }
-    const Rccl &R = rccl();
     if (h->local) {
         TRY(grow(h->d[0].device, reinterpret_cast<void **>(&h->lgathered), &h->lgathered_cap, s_total * 4));
     } else {
@@ -320,6 +331,7 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
             HIPT(hipSetDevice(h->d[0].device));
             return kth_internal_slots_sum(slot_bufs.data(), P, slot, h->d[0].stream);
         }
+        const Rccl &R = rccl();  // (the local transport never loads RCCL)
         NCCLT(R.GroupStart());
         for (Dev &x : h->d) {
             uint64_t *p = x.slots + (size_t)slot * KTH_STATS_WORDS;
@@ -341,6 +353,7 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
         TRY(kth_dist_sample(x.ctx, shards[i], shard_n[i], dst, s_dev[(size_t)i]));
     }
     if (!h->local) {
+        const Rccl &R = rccl();
         NCCLT(R.GroupStart());
         for (int i = 0; i < P; ++i) {
             Dev &x = h->d[(size_t)i];
@@ -360,40 +373,66 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
         }
         NCCLT(R.GroupEnd());
     }
+    // the window: on one device computed once and shared (every shard would
+    // derive the same one from the same gathered sample)
+    bool shared = false;
+    if (h->local) {
+        TRY(kth_dist_window(h->d[0].ctx, h->lgathered, s_total));
+        std::vector<kth_ctx *> rest;
+        for (int i = 1; i < P; ++i) rest.push_back(h->d[(size_t)i].ctx);
+        const int r = kth_internal_dist_window_share(h->d[0].ctx, rest.data(), P - 1);
+        TRY(r);
+        shared = r == KTH_OK;
+    }
     int slot = -1;
     for (int i = 0; i < P; ++i) {
         Dev &x = h->d[(size_t)i];
-        TRY(kth_dist_window(x.ctx, h->local ? h->lgathered : x.gathered, s_total));
+        if (!(shared || (h->local && i == 0)))
+            TRY(kth_dist_window(x.ctx, h->local ? h->lgathered : x.gathered, s_total));
         const int r = kth_dist_scan(x.ctx, shards[i], shard_n[i]);
         TRY(r);
         slot = r;
     }
     TRY(allreduce(slot));
-    for (int l = 0; l < KTH_DIST_LEVELS; ++l) {
+    // the levels, until every shard says KTH_DIST_DONE (they agree: the same
+    // reduced slots); usually one level, so two all-reduces in all
+    for (int l = 0;; ++l) {
         for (int i = 0; i < P; ++i) {
             const int r = kth_dist_level(h->d[(size_t)i].ctx, shards[i], shard_n[i], l);
             TRY(r);
+            if (i > 0 && r != slot) return KTH_EINTERNAL;
             slot = r;
         }
+        if (slot == KTH_DIST_DONE) break;
         TRY(allreduce(slot));
     }
     for (Dev &x : h->d) TRY(kth_dist_result(x.ctx, x.out));
+    // every shard's [answer, error] to the host in one gather per device and
+    // one wait each (a per-shard stats read and copy took ~2 round trips a shard)
+    if (h->local) {
+        std::vector<kth_ctx *> ctxs;
+        for (Dev &x : h->d) ctxs.push_back(x.ctx);
+        TRY(kth_internal_status_gather(ctxs.data(), P, h->d_status, h->d[0].stream));
+    } else {
+        for (int i = 0; i < P; ++i) {
+            Dev &x = h->d[(size_t)i];
+            TRY(kth_internal_status_gather(&x.ctx, 1, h->d_status + 2 * i, x.stream));
+        }
+    }
     h->enqueue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    for (Dev &x : h->d) {
+        if (h->local && &x != &h->d[0]) continue;  // (one shared stream)
+        HIPT(hipSetDevice(x.device));
+        HIPT(hipStreamSynchronize(x.stream));
+    }
     // every shard must hold the same answer (they picked the same digits from
     // the same reduced histograms); the per-shard error words must be clear
-    int32_t first = 0;
+    const volatile int32_t *hs = h->h_status;
     for (int i = 0; i < P; ++i) {
-        Dev &x = h->d[(size_t)i];
-        kth_stats st;
-        TRY(kth_ctx_last_stats(x.ctx, &st));  // synchronises x's stream
-        if (st.error != 0) return KTH_EINTERNAL;
-        int32_t a = 0;
-        HIPT(hipSetDevice(x.device));
-        HIPT(hipMemcpy(&a, x.out, 4, hipMemcpyDeviceToHost));
-        if (i == 0) first = a;
-        else if (a != first) return KTH_EINTERNAL;
+        if (hs[2 * i + 1] != 0) return KTH_EINTERNAL;
+        if (hs[2 * i] != hs[0]) return KTH_EINTERNAL;
     }
-    *out = first;
+    *out = hs[0];
     return KTH_OK;
 }
 

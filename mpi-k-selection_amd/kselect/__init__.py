@@ -23,7 +23,8 @@ import ctypes
 import numpy as np
 
 from ._lib import (  # noqa: F401
-    KTH_DIST_LEVELS,
+    KTH_DIST_DONE,
+    KTH_DIST_MAX_LEVELS,
     KTH_ECOMM,
     KTH_EINTERNAL,
     KTH_EINVAL,
@@ -151,6 +152,13 @@ class Selector:
         """Enqueue a select of device keys; the answer lands in device int32 *d_out."""
         check(LIB.kth_select_i32_async(self._ctx, _ptr(d_keys), int(n), int(k), _ptr(d_out)),
               "kth_select_i32_async")
+
+    def coop(self):
+        """True while the ctx runs the cooperative grid-barrier kernels (kth_ctx_coop)."""
+        r = LIB.kth_ctx_coop(self._ctx)
+        if r < 0:
+            check(r, "kth_ctx_coop")
+        return bool(r)
 
     def stats(self):
         st = KthStats()

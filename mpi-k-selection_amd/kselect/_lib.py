@@ -21,7 +21,8 @@ KTH_ECOMM = -6
 
 KTH_PATH_LDS, KTH_PATH_RADIX, KTH_PATH_WINDOW, KTH_PATH_WINDOW_FALLBACK = 1, 2, 3, 4
 KTH_STATS_WORDS = 8 + 2 * 2048
-KTH_DIST_LEVELS = 3
+KTH_DIST_DONE = 3  # kth_dist_level: no collective left, call kth_dist_result
+KTH_DIST_MAX_LEVELS = 3
 KTH_ROWS_MAX_COLS = 16384
 KTH_TOPK_MAX_COLS = 4096
 
@@ -85,6 +86,7 @@ PROTOS = {
     "kth_select_i32_ctx": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, c_i32p]),
     "kth_select_i32_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, c_vp]),
     "kth_ctx_last_stats": (ctypes.c_int, [c_vp, ctypes.POINTER(KthStats)]),
+    "kth_ctx_coop": (ctypes.c_int, [c_vp]),
     "kth_ctx_enable_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "kth_ctx_take_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]),

@@ -13,8 +13,9 @@ Replaces the CGM driver of the reference (TODO-kth-problem-cgm.c:76-278):
   :171-185 3-way count L/E/G                     ONE streaming pass per shard
   :190 MPI_Allreduce(3 ints)                     all_reduce of the counts
   :194-225 discard via VecErase                  local candidate compaction
-  :242-270 Gather sizes + Barrier + Gatherv      all_reduce of 2048-bin histograms,
-  :277-278 rank-0 qsort + VecGet(k-1)            one per 11-bit digit (3)
+  :242-270 Gather sizes + Barrier + Gatherv      the counts' all_reduce carries the candidates'
+  :277-278 rank-0 qsort + VecGet(k-1)            first 12-bit digit; one more all_reduce for the
+                                                 second (windows <= 2^24 values wide)
 
 Every rank ends with the same answer (the reference prints it on rank 0 only).
 The collectives never make the host wait between steps.  On GPUs they go
@@ -29,7 +30,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import KTH_DIST_LEVELS, KTH_EINTERNAL, KTH_STATS_WORDS, LIB as _lib, KthError, Selector, check, \
+from . import KTH_DIST_DONE, KTH_DIST_MAX_LEVELS, KTH_EINTERNAL, KTH_STATS_WORDS, LIB as _lib, KthError, Selector, check, \
     check_single_runtime
 from .rccl import RcclComm, TorchComm
 
@@ -144,11 +145,15 @@ class DistSelector:
         b.sample(shard, n_local, self._sample, s_local)
         yield ("all_gather", self._gathered, self._sample)
         b.window(self._gathered, s_local * self.world)
-        i = b.scan(shard, n_local)
+        i = b.scan(shard, n_local)  # counts + the candidates' first digit
         yield ("all_reduce", self.slots[i])
-        for level in range(KTH_DIST_LEVELS):
+        for level in range(KTH_DIST_MAX_LEVELS + 1):  # usually one level: two all-reduces in all
             i = b.level(shard, n_local, level)
+            if i == KTH_DIST_DONE:
+                break
             yield ("all_reduce", self.slots[i])
+        else:
+            raise KthError(KTH_EINTERNAL, "kth_dist_level never returned KTH_DIST_DONE")
         b.result(out)
 
     def select(self, shard, n_local, n_total, k, out=None):
@@ -163,6 +168,9 @@ class DistSelector:
         shard_bounds gives); below SMALL_PER_RANK keys per rank the shards are
         all-gathered and every rank selects from the union."""
         out = self.out if out is None else out
+        if self.comm is None:
+            raise RuntimeError("this DistSelector was built for lockstep() (world=P, no communicator); "
+                               "select() needs a process group")
         if n_total // self.world < SMALL_PER_RANK:
             if not (1 <= k <= n_total):
                 raise ValueError(f"k={k} outside [1, {n_total}]")
@@ -230,7 +238,8 @@ class DistSelector:
         return out
 
     def close(self):
-        self.comm.close()
+        if self.comm is not None:  # (lockstep selectors have none)
+            self.comm.close()
 
 
 def lockstep(selectors, shards, n_locals, k, outs=None, observe=None):

@@ -19,6 +19,9 @@ from kselect import LIB
 
 NCOUNTS, DIGIT, NBINS = 8, 11, 2048
 STATS_WORDS = NCOUNTS + 2 * NBINS
+DDIG, DNB = 12, 4096  # the sharded protocol's candidate / fallback digits (kth_kernels.hip DDIG)
+DONE_SLOT = 3  # KTH_DIST_DONE
+DIST_FULL_D0 = 32 - 2 * DDIG
 C_LT, C_EQLO, C_EQHI, C_IN, C_OVF = range(5)
 MAIN, CAND, FULL, DONE = "main", "cand", "full", "done"
 WINDOW_Z = float(LIB.kth_window_z())
@@ -45,6 +48,17 @@ def window_ranks(n, k, s):
 
 def cand_capacity(n):
     return int(LIB.kth_dist_cand_capacity(int(n)))
+
+
+def cand_domain(lo, hi):
+    """kth_kernels.hip cand_domain: keys lo < x < hi as x - base in [0, 2^W),
+    base = lo + 1; the first digit d0 bits, the later ones DDIG."""
+    base = (lo + 1) & 0xFFFFFFFF
+    if hi - lo < 2:
+        return base, 0, 0
+    W = (hi - lo - 2).bit_length()
+    nd = (W + DDIG - 1) // DDIG
+    return base, W, W - DDIG * (nd - 1 if nd else 0)
 
 
 def sample_indices(n_local, s_local):
@@ -84,6 +98,7 @@ class CpuBackend:
         slots.zero_()
         self.n, self.k = n_total, k
         self.mode = None
+        self.levels, self.result_slot = None, None
 
     def sample(self, shard, n_local, out, s_local):
         idx = sample_indices(n_local, s_local)
@@ -121,6 +136,8 @@ class CpuBackend:
         self.hi = int(srt[r_hi - 1]) if a1 else 0xFFFFFFFF
 
     def scan(self, shard, n_local):
+        """k_main<0> (counts, candidates) + k_dscan_hist (the candidates'
+        first digit into the same slot)."""
         u = shard.numpy()[:n_local].view(np.uint32) ^ np.uint32(0x80000000)
         lo, hi = np.uint32(self.lo), np.uint32(self.hi)
         inside = (u > lo) & (u < hi)
@@ -133,19 +150,23 @@ class CpuBackend:
         s0[C_IN] = int(inside.sum())
         s0[C_OVF] = 1 if self.cand.size > cap else 0
         self.keys = u
+        base, W, d0 = cand_domain(self.lo, self.hi)
+        if W and self.cand.size:
+            v = (self.cand[:cap].astype(np.uint64) - np.uint64(base)) & np.uint64(0xFFFFFFFF)
+            bins = (v >> np.uint64(W - d0)) & np.uint64((1 << d0) - 1)
+            s0[NCOUNTS:NCOUNTS + DNB] = torch.from_numpy(np.bincount(bins.astype(np.int64), minlength=DNB))
         return 0
 
     def _decide(self, c):
+        """kth_kernels.hip decide_dist."""
         L, E1, E2r, M, ovf = (int(x) for x in c[:5])
         E2 = 0 if self.lo == self.hi else E2r
         k = self.k
-        self.base, self.W, self.prefix, self.done, self.kr = 0, 32, 0, 0, k
+        self.base, self.W, self.d0, self.prefix, self.done, self.kr = 0, 32, 0, 0, 0, k
         if L < k <= L + E1:
             self.mode, self.answer = DONE, self.lo
         elif L + E1 < k <= L + E1 + M and ovf == 0:
-            self.base = (self.lo + 1) & 0xFFFFFFFF
-            rng = (self.hi - self.lo - 2) & 0xFFFFFFFF
-            self.W = rng.bit_length()
+            self.base, self.W, self.d0 = cand_domain(self.lo, self.hi)
             self.kr = k - L - E1
             self.mode = CAND
             if self.W == 0:
@@ -153,14 +174,20 @@ class CpuBackend:
         elif L + E1 + M < k <= L + E1 + M + E2:
             self.mode, self.answer = DONE, self.hi
         else:
-            self.mode = FULL
+            self.mode, self.d0 = FULL, DIST_FULL_D0
         self.path = "fallback" if self.mode == FULL else "window"
 
+    def _live(self):
+        return self.mode in (CAND, FULL) and self.done < self.W
+
+    def _digit(self):
+        return min(self.d0 if self.done == 0 else DDIG, self.W - self.done)
+
     def _pick(self, slot):
-        if self.mode not in (CAND, FULL) or self.done >= self.W:
+        if not self._live():
             return
-        d = min(DIGIT, self.W - self.done)
-        h = slot[NCOUNTS:NCOUNTS + NBINS].numpy()
+        d = self._digit()
+        h = slot[NCOUNTS:NCOUNTS + DNB].numpy()
         cum = np.cumsum(h)
         b = int(np.searchsorted(cum, self.kr, side="left"))
         assert b < (1 << d), "histogram holds fewer than k keys"
@@ -173,27 +200,39 @@ class CpuBackend:
 
     def _hist(self, slot):
         slot.zero_()
-        if self.mode not in (CAND, FULL) or self.done >= self.W:
+        if not self._live():
             return
         dom = self.cand if self.mode == CAND else self.keys
         v = (dom.astype(np.uint64) - np.uint64(self.base)) & np.uint64(0xFFFFFFFF)
-        d = min(DIGIT, self.W - self.done)
+        d = self._digit()
         if self.done:
             v = v[(v >> np.uint64(self.W - self.done)) == np.uint64(self.prefix)]
         bins = (v >> np.uint64(self.W - self.done - d)) & np.uint64((1 << d) - 1)
-        slot[NCOUNTS:NCOUNTS + NBINS] = torch.from_numpy(np.bincount(bins.astype(np.int64), minlength=NBINS))
+        slot[NCOUNTS:NCOUNTS + DNB] = torch.from_numpy(np.bincount(bins.astype(np.int64), minlength=DNB))
 
     def level(self, shard, n_local, level):
+        """k_dlevel: level 0 decides and picks the first digit from the scan's
+        slot, and counts the level calls that return a slot (DistStatus);
+        later levels pick; each histograms the next digit; KTH_DIST_DONE once
+        no digit is left."""
         U = self.slots
+        if level >= 1 and level >= self.levels:
+            self.result_slot = level % 3
+            return DONE_SLOT
         src, acc = U[level % 3], U[(level + 1) % 3]
         if level == 0:
             self._decide(src)
+            if self.mode == CAND:
+                self._pick(src)
         else:
             self._pick(src)
+        if level == 0:
+            left = self.W - self.done - self._digit() if self._live() else 0
+            self.levels = 1 + (left + DDIG - 1) // DDIG
         self._hist(acc)
         return (level + 1) % 3
 
     def result(self, out):
-        self._pick(self.slots[0])
+        self._pick(self.slots[self.result_slot])
         assert self.mode == DONE, self.mode
         out[0] = int(np.uint32(self.answer ^ 0x80000000).view(np.int32))

@@ -1,7 +1,10 @@
 """The sharded C drop-in for the reference CGM driver (apps/kth_cgm.c):
-`mpirun -n P kth_cgm n k --input keys.bin` must print the reference's output
-line (TODO-kth-problem-cgm.c:280) with the true k-th smallest, which the
-golden fixtures pin to the reference's own mpirun answers.
+`mpirun -n P kth_cgm n k --input keys.bin` must print one of the reference's
+two output lines with the true k-th smallest, which the golden fixtures pin to
+the reference's own mpirun answers: "kth element %d\n time: %f\n"
+(TODO-kth-problem-cgm.c:289, the reference's pivot found by its 3-way count)
+when the answer is a window edge decided from the all-reduced counts, else
+"kth element=%d \ntime: %f\n" (:280, after the final gather + solve).
 
 CPU: the binary exists and fails loudly without a GPU (no CPU fallback).
 GPU: P = 1 (RCCL communicator) and P = 2 (two ranks share the one GPU, so the
@@ -18,7 +21,17 @@ from conftest import GOLDEN, PKG
 
 BIN = os.path.join(os.environ.get("KTH_BIN_DIR") or os.path.join(PKG, "bin"), "kth_cgm")
 MPIRUN = "/opt/conda/bin/mpirun"
-OUT = re.compile(r"kth element=(-?\d+) \ntime: ([0-9.]+)\n")
+OUT_280 = re.compile(r"kth element=(-?\d+) \ntime: ([0-9.]+)\n")   # TODO-kth-problem-cgm.c:280
+OUT_289 = re.compile(r"kth element (-?\d+)\n time: ([0-9.]+)\n")    # TODO-kth-problem-cgm.c:289
+
+
+def parse(stdout):
+    """(answer, time, line) from the driver's output: line 280 or 289."""
+    for line, rx in ((280, OUT_280), (289, OUT_289)):
+        m = rx.search(stdout)
+        if m:
+            return int(m.group(1)), float(m.group(2)), line
+    return None
 
 needs_mpi = pytest.mark.skipif(not (os.path.exists(BIN) and os.path.exists(MPIRUN)),
                                reason="kth_cgm or mpirun not available")
@@ -56,21 +69,26 @@ def _pick(c):
 @needs_mpi
 @pytest.mark.parametrize("p", [1, 2])
 def test_cgm_driver_golden(golden, p):
-    seen = 0
+    seen, line_of = 0, {}
     for c in golden["cases"]:
         if not _pick(c):
             continue
         r = run(p, c["n"], c["k"], "--input", os.path.join(GOLDEN, "inputs", c["input"]))
         assert r.returncode == 0, r.stderr[-2000:]
-        m = OUT.search(r.stdout)
-        assert m, r.stdout
-        got = int(m.group(1))
+        res = parse(r.stdout)
+        assert res, r.stdout
+        got, _, line = res
         assert got == c["true"], (c, p, got)
         ref = c["cgm_ref"].get(str(max(p, 2)))
         if ref not in (None, "livelock"):
             assert got == ref, (c, p, got, ref)
+        line_of[(c["family"], c["n"], {1: "first", c["n"]: "last"}.get(c["k"], "mid"))] = line
         seen += 1
     assert seen >= 8
+    # all keys equal: the window is the one value, decided from the counts (:289);
+    # distinct full-range keys: the median lies strictly inside the window (:280)
+    assert line_of[("all_equal", 16384, "mid")] == 289, line_of
+    assert line_of[("uniform_full", 16384, "mid")] == 280, line_of
 
 
 @pytest.mark.gpu
@@ -81,5 +99,5 @@ def test_cgm_driver_generated_checked(p, extra):
     window path on every rank, verified by a sort on rank 0, plus repeats."""
     r = run(p, 1 << 22, 0, 12345, "--median", "--check", "--repeat", 3, *extra, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert OUT.search(r.stdout), r.stdout
+    assert parse(r.stdout), r.stdout
     assert "check: ok" in r.stderr and "device-resident select" in r.stderr, r.stderr

@@ -217,10 +217,49 @@ def test_lockstep_slots_match_cpu_p8(gpu, fam):
                 og = lockstep(hd, dsh, sizes, k, observe=lambda kind, x: seen_g.append((kind, x.cpu().clone())))
                 oc = lockstep(cd, csh, sizes, k, observe=lambda kind, x: seen_c.append((kind, x.clone())))
                 torch.cuda.synchronize()
-                assert len(seen_g) == len(seen_c) == 5
+                # one all-gather, then 2 all-reduces (window <= 2^24 wide, or
+                # decided by the counts), 3 (wider) or 4 (the exact fallback)
+                assert len(seen_g) == len(seen_c) and 3 <= len(seen_g) <= 5, (len(seen_g), len(seen_c))
                 for (kg, xg), (kc, xc) in zip(seen_g, seen_c):
                     assert kg == kc and torch.equal(xg, xc), (fam, sizes, k, kg)
                 assert {int(o.item()) for o in og} == {int(o[0]) for o in oc} == {int(srt[k - 1])}, (fam, k)
+    finally:
+        for s in sels:
+            s.close()
+
+
+@pytest.mark.parametrize("fam", ["uniform_half", "few_distinct"])
+def test_lockstep_two_allreduces_p8(gpu, fam):
+    """The protocol's common case: P = 8 shards of a 2^26-key input whose window
+    is at most 2^24 values wide (uniform half-range keys, the bench's family)
+    or decided by its counts (few distinct values) -- one all-gather and TWO
+    all-reduces, device and CPU restatement slot for slot."""
+    import torch
+    from dist_cpu_backend import CpuBackend
+    from kselect import Selector
+    from kselect.dist import DistSelector, HipBackend, lockstep
+    n = 1 << 26
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu.fill(t, n, fam, param=7)
+    gpu.sync()
+    host = t.cpu()
+    sizes = [n // 8] * 8
+    dsh = [t[i * (n // 8):(i + 1) * (n // 8)] for i in range(8)]
+    csh = [host[i * (n // 8):(i + 1) * (n // 8)] for i in range(8)]
+    k = n // 2
+    want = int(torch.kthvalue(host, k).values)
+    sels = [Selector(0) for _ in range(8)]
+    try:
+        seen_g, seen_c = [], []
+        og = lockstep([DistSelector(HipBackend(0, s), world=8) for s in sels], dsh, sizes, k,
+                      observe=lambda kind, x: seen_g.append((kind, x.cpu().clone())))
+        oc = lockstep([DistSelector(CpuBackend(), world=8) for _ in range(8)], csh, sizes, k,
+                      observe=lambda kind, x: seen_c.append((kind, x.clone())))
+        torch.cuda.synchronize()
+        assert [kd for kd, _ in seen_g] == [kd for kd, _ in seen_c] == ["all_gather", "all_reduce", "all_reduce"]
+        for (kg, xg), (kc, xc) in zip(seen_g, seen_c):
+            assert torch.equal(xg, xc), (fam, kg)
+        assert {int(o.item()) for o in og} == {int(o[0]) for o in oc} == {want}
     finally:
         for s in sels:
             s.close()

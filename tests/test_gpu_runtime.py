@@ -143,6 +143,35 @@ def faulty():
     f.close()
 
 
+def test_coop_backoff_counts_every_entry_point(gpu):
+    """One grid-barrier timeout (KTH_FAULT_BARRIER=once) turns the cooperative
+    kernels off for COOP_BACKOFF = 64 selections; asynchronous selects count
+    down too, so a ctx used only asynchronously afterwards gets them back."""
+    import torch
+    import kselect
+    os.environ["KTH_FAULT_BARRIER"] = "once"
+    try:
+        sel = kselect.Selector(0)
+    finally:
+        del os.environ["KTH_FAULT_BARRIER"]
+    try:
+        n = (1 << 24) + 3
+        keys, srt = _keys(gpu, n, "uniform_full")
+        assert sel.coop()
+        assert sel.select(keys, n // 2) == srt[n // 2 - 1]  # times out once, redone per level
+        assert not sel.coop()
+        out = torch.zeros(1, dtype=torch.int32, device="cuda")
+        for i in range(63):
+            sel.select_async(keys, n, n // 3, out)
+            assert not sel.coop(), i
+        sel.select_async(keys, n, n // 3, out)  # the 64th: cooperative again
+        assert sel.coop()
+        sel.sync()
+        assert int(out.item()) == srt[n // 3 - 1] and sel.stats()["error"] == 0
+    finally:
+        sel.close()
+
+
 @pytest.mark.parametrize("n", [(1 << 20) + 7, (1 << 24) + 3])  # radix path (k_finish only), window path
 def test_barrier_timeout_reported_and_out_untouched(gpu, faulty, n):
     import torch

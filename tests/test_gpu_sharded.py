@@ -84,6 +84,7 @@ def test_dist_backend_slots_match(gpu, fam):
     step on the same shard at world 1: same sample, same slots, same answer."""
     import torch
     from dist_cpu_backend import CpuBackend
+    from kselect import KTH_DIST_DONE, KTH_DIST_MAX_LEVELS
     from kselect.dist import HipBackend
     n = (1 << 23) + 77
     keys = _dev_keys(gpu, n, fam)
@@ -105,10 +106,15 @@ def test_dist_backend_slots_match(gpu, fam):
         i, j = hb.scan(keys, n), cb.scan(host, n)
         torch.cuda.synchronize()
         assert i == j and torch.equal(sg[i].cpu(), sc[j]), (fam, k, "scan", sg[i][:5].tolist(), sc[j][:5].tolist())
-        for level in range(3):
+        for level in range(KTH_DIST_MAX_LEVELS + 1):  # until KTH_DIST_DONE (the same call on both)
             i, j = hb.level(keys, n, level), cb.level(host, n, level)
             torch.cuda.synchronize()
-            assert i == j and torch.equal(sg[i].cpu(), sc[j]), (fam, k, "level", level)
+            assert i == j, (fam, k, "level", level, i, j)
+            if i == KTH_DIST_DONE:
+                break
+            assert torch.equal(sg[i].cpu(), sc[j]), (fam, k, "level", level)
+        else:
+            raise AssertionError("no KTH_DIST_DONE")
         og, oc = hb.alloc_out(), cb.alloc_out()
         hb.result(og)
         cb.result(oc)
