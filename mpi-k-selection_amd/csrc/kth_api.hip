@@ -54,7 +54,10 @@ constexpr size_t HSLOT_OFF = ISLOT_WORDS;
 constexpr size_t HSLOT_WORDS = (size_t)kth::HEAD_LEVELS * kth::STATS_WORDS;
 constexpr size_t FSLOT_OFF = HSLOT_OFF + HSLOT_WORDS;  // two sets, alternate k_finish launches
 constexpr size_t FSLOT_WORDS = (size_t)kth::FIN_LEVELS * kth::STATS_WORDS;
-constexpr size_t ZERO_WORDS = FSLOT_OFF + 2 * FSLOT_WORDS;
+constexpr size_t PRE_OFF = FSLOT_OFF + 2 * FSLOT_WORDS;  // two PreHist sets (u32 words), alternate selects
+constexpr size_t PRE_SET_WORDS = (size_t)kth::PRE_WORDS / 2;  // (in u64 words)
+static_assert(kth::PRE_WORDS % 4 == 0, "PreHist sets stay 16-byte aligned");
+constexpr size_t ZERO_WORDS = PRE_OFF + 2 * PRE_SET_WORDS;
 constexpr size_t BAR_OFF = ZERO_WORDS;
 constexpr size_t TAIL_OFF = BAR_OFF + kth::BAR_WORDS / 2;  // k_finish's tail keys (FIN_LDS_KEYS u32)
 constexpr size_t SLOT_ALLOC_WORDS = TAIL_OFF + kth::FIN_LDS_KEYS / 2;
@@ -66,7 +69,7 @@ constexpr int MAX_EVENTS = 4 * 2048;
 constexpr u64 TK_STAGE_MAX_FRAC = 16;  // staged top-k (k_main<5/6>) for k <= n / 16
 constexpr int TK5_SPLIT = 4;            // workgroups per k_main workgroup in k_tk5_count / k_tk5_write (window-parallel)
 constexpr int COOP_BACKOFF = 64;        // synchronous selects on the per-level path after a grid-barrier timeout
-constexpr uint64_t DSCAN_PER_WG = 1ull << 15;  // candidates per workgroup of the sharded scan's first-digit histogram
+constexpr uint64_t DSCAN_PER_WG = 1ull << 16;  // candidates per workgroup of the sharded scan's first-digit histogram
 
 #define HIP_TRY(x)                                                                                    \
     do {                                                                                              \
@@ -103,6 +106,7 @@ struct kth_ctx {
     int fin_grid = 256;        // k_finish workgroups (one per CU; KTH_FIN_GRID)
     uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
     int fin_set = 0;           // k_finish slot set of the next launch (the other one is cleared by it)
+    bool pre_hist = true;      // k_main<0> histograms the candidates' first digit for k_finish (KTH_PRE_HIST=0: off)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -374,13 +378,21 @@ kth::CoopArgs coop_args(kth_ctx *c, u64 slot_off, int32_t *d_out, int32_t *d_sta
 // k_finish: the finish phase in one launch, on slot set fin_set; it clears the
 // other set and the sample phase's slots for the next select
 constexpr size_t FIN_DYN_LDS = (size_t)kth::FIN_LDS_KEYS * 4;
-void launch_finish(kth_ctx *c, StepArgs a, int32_t *d_out, int32_t *d_status) {
+uint32_t *pre_set(kth_ctx *c, int set) {
+    return reinterpret_cast<uint32_t *>(c->islots + PRE_OFF + (size_t)set * PRE_SET_WORDS);
+}
+
+// with_pre: this select's k_main<0> histogrammed the candidates' first digit
+// into PreHist set fin_set
+void launch_finish(kth_ctx *c, StepArgs a, int32_t *d_out, int32_t *d_status, bool with_pre = false) {
     const size_t mine = FSLOT_OFF + (size_t)c->fin_set * FSLOT_WORDS;
     a.stats_zero = c->islots + FSLOT_OFF + (size_t)(1 - c->fin_set) * FSLOT_WORDS;
     a.zero_words = FSLOT_WORDS;
     kth::CoopArgs x = coop_args(c, mine, d_out, d_status);
     x.zero2 = c->islots + HSLOT_OFF;
     x.zero2_words = HSLOT_WORDS;
+    x.pre = with_pre ? pre_set(c, c->fin_set) : nullptr;
+    x.pre_zero = pre_set(c, 1 - c->fin_set);
     kth::k_finish<<<c->fin_grid, kth::DENSE_BLK, FIN_DYN_LDS, c->stream>>>(a, x);
     c->fin_set ^= 1;
 }
@@ -460,10 +472,13 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
         a.r_hi = r_hi;
         kth::k_head<<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, coop_args(c, HSLOT_OFF, nullptr, nullptr),
                                                                           keys, (u64)n, stride, c->sample, (u64)s);
-        // the streaming pass: counts into islot(1) (zero between selects)
+        // the streaming pass: counts into islot(1) (zero between selects);
+        // the plain pass also histograms the candidates' first digit for k_finish
         a = step(c, kth::ADV_CARRY, 0, 1, nullptr, islot(c, 1), nullptr);
         a.keys = keys;
         a.n_local = (u64)n;
+        const bool pre = tflag == 0 && c->pre_hist;
+        if (pre) a.pre_hist = pre_set(c, c->fin_set);
         ev_main(c);
         launch_main(c, a, tflag, tflags);
         ev_main(c);
@@ -471,7 +486,7 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
         a = step(c, kth::ADV_DECIDE, 1, 0, islot(c, 1), nullptr, nullptr);
         a.keys = keys;
         a.n_local = (u64)n;
-        launch_finish(c, a, d_out, d_status);
+        launch_finish(c, a, d_out, d_status, pre);
         c->last_state = 0;
         c->counts_left = true;  // (k_head clears them; a sharded select on this ctx must too)
         return launch_check();
@@ -696,6 +711,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             if (const char *g = getenv("KTH_POST_DENSE_GRID")) c->post_dense_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_COOP")) c->coop = atoi(g) != 0;
+            if (const char *g = getenv("KTH_PRE_HIST")) c->pre_hist = atoi(g) != 0;
             c->fin_grid = c->num_cu;
             if (const char *g = getenv("KTH_FIN_GRID")) c->fin_grid = std::max(1, std::min(atoi(g), c->num_cu));
             if (const char *g = getenv("KTH_HEAD_SLACK")) c->head_slack64 = (uint32_t)std::max(0.0, atof(g) * 64.0);

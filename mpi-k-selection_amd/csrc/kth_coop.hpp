@@ -44,6 +44,8 @@ struct CoopArgs {
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
     uint32_t sample_ready;  // k_head: the sample (order keys) is already in `sample` (sharded window)
     uint32_t fault;    // test hook (KTH_FAULT_BARRIER): the grid barriers report a timeout
+    const uint32_t *pre;  // k_finish: k_main<0>'s first candidate digit (PreHist), or null
+    uint32_t *pre_zero;   // k_finish: the other PreHist set, cleared for the next select
 };
 
 // This wave's outstanding global accesses (atomics, write-through stores) are
@@ -157,6 +159,25 @@ __device__ __forceinline__ void pick_slot_copies(SelState &ss, const u64 *slot, 
         h0[j] = sum;
     }
     __syncthreads();
+    pick_state<BLOCK, PER>(ss, h0, h0, true, scratch, nullptr, cnt0);
+}
+
+// The first candidate digit from k_main<0>'s PreHist (nb <= PRE_BINS bins in
+// PRE_COPIES copies; written by the previous kernel: plain loads), summed per
+// bin, and picked (target 0).
+template <int BLOCK>
+__device__ __forceinline__ void pick_pre(SelState &ss, const uint32_t *pre, uint32_t nb, u64 *scratch, u64 *cnt0) {
+    constexpr int PER = NBINS / BLOCK;
+    u64 h0[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t b = threadIdx.x * PER + j;
+        uint32_t sum = 0;
+        if (b < nb)
+#pragma unroll 4
+            for (int c = 0; c < PRE_COPIES; ++c) sum += pre[c * PRE_BINS + b];
+        h0[j] = sum;
+    }
     pick_state<BLOCK, PER>(ss, h0, h0, true, scratch, nullptr, cnt0);
 }
 
@@ -347,14 +368,15 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
 //   * The first digit is 9 bits wide (FIN_D0; wider only when W > 30 needs
 //     it): every key of the domain lands in it, so every workgroup flushes
 //     nearly all of its bins -- 512 global atomics a workgroup into 4 copies,
-//     not 2048 onto one.  The later digits only see the keys of one bin, and
+//     not 2048 onto one.  When k_main<0> has histogrammed it already
+//     (x.pre, PreHist: complete unless a workgroup flushed its staging
+//     mid-pass), it is picked from there: no histogram, flush or barrier.  The later digits only see the keys of one bin, and
 //     once that bin fits one workgroup's LDS, finish_tail ends the launch.
 //   * Slots come in two sets used by alternate launches (x.slots: this
 //     launch's, a.stats_zero: the other set, cleared here for the next one),
 //     and the sample phase's slots (x.zero2) are cleared here too: no barrier
 //     after the last level.
 constexpr int FIN_LDS_KEYS = 32768;  // LDS-resident keys per workgroup (128 KiB of dynamic LDS)
-constexpr uint32_t FIN_D0 = 9;  // [257, 512] bins used: ~12-25 K keys a bin from 6.3 M candidates
 constexpr int FIN_UNROLL = 4;        // 16-B loads in flight per thread (1024-thread workgroups: <= 128 VGPRs)
 
 __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPlan &plan, const uint4 &x, bool xr,
@@ -588,10 +610,13 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
     KTH_STAMP(a, 0);
     GridBar gb = grid_bar_init(x.bar, s_base);
     for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
+    const uint32_t pre_incomplete = x.pre ? x.pre[PRE_INCOMPLETE] : 1u;  // (loaded beside the state)
     advance<DENSE_BLK>(ss, a, scratch);
     if (threadIdx.x == 0 && (ss.mode == MODE_CAND || ss.mode == MODE_FULL) && ss.t[0].done == 0)
-        ss.d0 = ss.W > 30u ? ss.W - 22u : FIN_D0;
+        ss.d0 = fin_first_digit(ss.W);
     __syncthreads();
+    // the candidates' first digit from k_main (grid-uniform: every workgroup reads the same words)
+    const bool use_pre = pre_incomplete == 0u && ss.mode == MODE_CAND && ss.t[0].done == 0;
     KTH_STAMP(a, 1);
     // the domain (block-uniform): candidates or the input, and this workgroup's slice
     const uint32_t mode0 = ss.mode;
@@ -618,9 +643,10 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
                 reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
             __syncthreads();
         }
+        const bool pre0 = L == 0 && use_pre;  // the digit is picked from PreHist below
         if (resident) {
             const uint32_t nv = (uint32_t)((nk + 3) / 4);
-            if (L == 0) {  // HBM -> registers -> histogram + LDS
+            if (L == 0) {  // HBM -> registers -> histogram + LDS (pre0: LDS only)
                 // the domain's first digit: one target, no prefix yet, so a full
                 // vector's keys cost a subtract, a shift and an LDS atomic each
                 // (hist_add's generic two-target path was ~2x the VALU issue)
@@ -647,7 +673,9 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
                             if (v < nv) {
                                 const u64 e = 4ull * v;
                                 res[v] = q[u];
-                                if (one && nk - e >= 4)
+                                if (pre0)
+                                    ;  // (the digit comes from PreHist)
+                                else if (one && nk - e >= 4)
                                     add4(q[u]);
                                 else
                                     finish_keys(lh, plan, q[u], xr, nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u);
@@ -663,7 +691,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
                         if (left > 2) q.z = dom[e + 2];
                         if (left > 3) q.w = dom[e + 3];
                         res[v] = q;
-                        finish_keys(lh, plan, q, xr, left >= 4 ? 0xFu : (1u << (uint32_t)left) - 1u);
+                        if (!pre0) finish_keys(lh, plan, q, xr, left >= 4 ? 0xFu : (1u << (uint32_t)left) - 1u);
                     }
                 }
             } else {  // the slice from LDS
@@ -672,7 +700,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
                     finish_keys(lh, plan, res[v], xr, nk - e >= 4 ? 0xFu : (1u << (uint32_t)(nk - e)) - 1u);
                 }
             }
-        } else {
+        } else if (!pre0) {
             // streamed from HBM every level (a domain larger than the grid's LDS)
             const uint32_t active = active_wgs(count, L == 0 ? x.dense_per_wg : x.sparse_per_wg);
             auto f = [&](const uint32_t *k, uint32_t valid, auto full) {
@@ -691,18 +719,22 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         // first digit: every key lands, so every workgroup flushes nearly every
         // bin -- into NBINS / bins copies; later digits see one bin's keys
         const uint32_t nb = plan.mask[0] + 1u, copies = L == 0 ? NBINS / nb : 1u;
-        if (copies > 1)
-            hist_flush_copies<DENSE_BLK>(lh, nb, copies, slot);
-        else
-            hist_flush<DENSE_BLK>(lh, plan, slot);
-        if (L == 0) KTH_STAMP(a, 2);
-        grid_sync(gb, s_base, ok);
-        if (x.fault) ok = false;  // test hook: as if this barrier had timed out
-        if (L == 0) KTH_STAMP(a, 3);
-        if (copies > 1)
-            pick_slot_copies<DENSE_BLK>(ss, slot, nb, copies, reinterpret_cast<u64 *>(&lh[0][0]), scratch, &s_cnt0);
-        else
-            pick_slot<DENSE_BLK>(ss, slot, share, scratch, nullptr, &s_cnt0);
+        if (pre0) {
+            pick_pre<DENSE_BLK>(ss, x.pre, nb, scratch, &s_cnt0);
+        } else {
+            if (copies > 1)
+                hist_flush_copies<DENSE_BLK>(lh, nb, copies, slot);
+            else
+                hist_flush<DENSE_BLK>(lh, plan, slot);
+            if (L == 0) KTH_STAMP(a, 2);
+            grid_sync(gb, s_base, ok);
+            if (x.fault) ok = false;  // test hook: as if this barrier had timed out
+            if (L == 0) KTH_STAMP(a, 3);
+            if (copies > 1)
+                pick_slot_copies<DENSE_BLK>(ss, slot, nb, copies, reinterpret_cast<u64 *>(&lh[0][0]), scratch, &s_cnt0);
+            else
+                pick_slot<DENSE_BLK>(ss, slot, share, scratch, nullptr, &s_cnt0);
+        }
         KTH_STAMP(a, 4 + L);
         // a small bin left: the last workgroup to arrive finishes alone (block-uniform)
         if (resident && (ss.mode == MODE_CAND || ss.mode == MODE_FULL) && s_cnt0 <= (u64)FIN_LDS_KEYS) {
@@ -735,6 +767,9 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
         a.stats_zero[i] = 0;
     for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < x.zero2_words; i += (u64)gridDim.x * DENSE_BLK)
         x.zero2[i] = 0;
+    if (x.pre_zero)
+        for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < (u64)PRE_WORDS; i += (u64)gridDim.x * DENSE_BLK)
+            x.pre_zero[i] = 0u;
     KTH_STAMP(a, 7);
 }
 

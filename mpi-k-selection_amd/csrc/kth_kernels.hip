@@ -74,7 +74,29 @@ struct StepArgs {
     uint32_t *host_status; // k_dlevel, level 0 of the sharded protocol: DistStatus in host-visible memory
     uint32_t tag;          // ... with this tag (the host's call counter)
     u64 dense_per_wg;      // k_dlevel: keys per active workgroup for a domain's first digit
+    uint32_t *pre_hist;    // k_main<0> (single-GPU window path): the candidates' first digit (PreHist), or null
 };
+
+// k_finish's first candidate digit: FIN_D0 bits ([257, 512] bins used: ~12-25 K
+// keys a bin from 6.3 M candidates at 2^30), wider only when W > 30 needs it
+constexpr uint32_t FIN_D0 = 9;
+__host__ __device__ __forceinline__ uint32_t fin_first_digit(uint32_t W) { return W > 30u ? W - 22u : FIN_D0; }
+
+// The candidates' first digit, histogrammed by k_main<0> at the end of each
+// workgroup from its waves' staging regions (every candidate of a workgroup
+// is still there unless a wave had to flush its region mid-pass, which the
+// workgroup then reports in `incomplete` instead), into PRE_COPIES copies
+// (workgroup b adds to copy b % PRE_COPIES: 64 same-address adders a bin, not
+// 1024).  k_finish picks the digit from it without a histogram pass, a flush
+// or a grid barrier.  Two sets, alternate selects (k_finish clears the other).
+constexpr int PRE_COPIES = 16, PRE_BINS = 1024;  // a first digit of at most 10 bits (W <= 32)
+constexpr int PRE_WORDS = PRE_COPIES * PRE_BINS + 64;  // u32: the copies, then `incomplete` (own 256-B line)
+constexpr int PRE_INCOMPLETE = PRE_COPIES * PRE_BINS;
+// the candidate domain of k_finish's decide(): v = key - (lo + 1) in [0, 2^W)
+__device__ __forceinline__ uint32_t cand_width(uint32_t lo, uint32_t hi) {
+    const uint32_t range = hi - lo - 2u;
+    return range ? 32u - (uint32_t)__clz(range) : 0u;
+}
 
 // Diagnostic phase stamps (KTH_STAMPS=1 only; null pointer in the product):
 // thread 0 of each workgroup records the 100 MHz wall clock at point i.
@@ -603,6 +625,7 @@ struct Stager {
     u64 *cand_count, *acc, cap;
     uint32_t *cand_out;
     uint32_t *rows_out;  // ROWS only
+    uint32_t flushed;    // wave-uniform: the region was flushed mid-pass (its keys left LDS)
 
     // the region's first `cnt` keys (and rows) to candidates [g, g + cnt)
     __device__ __forceinline__ void put(u64 g, uint32_t cnt) const {
@@ -620,6 +643,7 @@ struct Stager {
         put(g, wfill);
         __builtin_amdgcn_wave_barrier();
         wfill = 0;
+        flushed = 1u;
     }
 
     // One key slot of the wave, as the streaming pass sees it: `near` = this
@@ -1019,7 +1043,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
             tflags[2] = 1u;
         }
     }
-    Stager<ROWS> st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out, cand_rows};
+    Stager<ROWS> st{region[wid], 0u, 0ull, a.cand_count, a.stats_acc, a.cap, cand_out, cand_rows, 0u};
     OrdStager os{region[wid], 0u, 0u, 0ull, ((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.cap, slo, shi,
                  a.cand_count, a.stats_acc, a.cap, cand_out, seg};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
@@ -1270,6 +1294,34 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         u64 g = red[5][0];
         for (int w = 0; w < wid; ++w) g += red[4][w];
         st.put(g, st.wfill);
+    }
+    if constexpr (TF == 0) {
+        if (a.pre_hist) {  // kernel-uniform: the candidates' first digit for k_finish (PreHist)
+            __shared__ uint32_t phist[PRE_BINS];
+            __shared__ uint32_t pflushed;
+            const uint32_t W = cand_width(ss.lo, ss.hi);
+            const uint32_t d = min(W, fin_first_digit(W)), sh = W - d, base = ss.lo + 1u;
+            if (threadIdx.x == 0) pflushed = 0u;
+            for (int b = threadIdx.x; b < PRE_BINS; b += BLK) phist[b] = 0u;
+            __syncthreads();
+            if (lane == 0 && st.flushed) atomicOr(&pflushed, 1u);
+            __syncthreads();
+            if (pflushed) {  // block-uniform: some of its candidates left LDS
+                if (threadIdx.x == 0) atomicAdd(&a.pre_hist[PRE_INCOMPLETE], 1u);
+            } else if (W > 0u) {
+#pragma unroll
+                for (int q = 0; q < BLK / WAVE; ++q) {
+                    const uint32_t nq = (uint32_t)red[4][q];
+                    for (uint32_t i = threadIdx.x; i < nq; i += BLK) atomicAdd(&phist[(region[q][i] - base) >> sh], 1u);
+                }
+                __syncthreads();
+                uint32_t *dst = a.pre_hist + (blockIdx.x % PRE_COPIES) * PRE_BINS;
+                for (uint32_t b = threadIdx.x; b < (1u << d); b += BLK) {
+                    const uint32_t c = phist[b];
+                    if (c) atomicAdd(&dst[b], c);
+                }
+            }
+        }
     }
     KTH_STAMP(a, 5);
 }

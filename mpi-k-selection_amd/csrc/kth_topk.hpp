@@ -269,6 +269,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 // every kept key its slot in the tile's output range, which is contiguous:
 // [bb + min(be, need), + #better + #kept ties).  The pairs are staged in the
 // wave's LDS and written out coalesced.
+#ifndef KTH_TKW_TILES
+#define KTH_TKW_TILES 2
+#endif
+constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
 template <bool ALIGNED, bool STAGED = false>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
@@ -299,70 +303,88 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
         }
         const bool act = tl >= t_from && (tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need));
         u64 todo = __ballot(act);
+        // TKW_TILES tiles a round: all their loads in flight together (one
+        // tile's 4 KiB a wave left the loads idle while the tile was placed
+        // and copied out)
         while (todo) {
-            const int src = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const u64 t = tg + src;
-            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, src);
-            const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), src) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
-            const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
-            const u64 ce = tk_equal_of(c);
-            const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
-            const uint32_t total = tk_better_of(c) + (uint32_t)take_e;  // this tile's output keys
-            const u64 start = bb + (be < need ? be : need);            // and where they go
-            const u64 i0 = t * TK_TILE + (u64)lane * TK_KPL;
-            uint32_t x[TK_KPL];
-            if (ALIGNED && t * TK_TILE + TK_TILE <= n) {
+            u64 t[TKW_TILES];
+            bool has[TKW_TILES];
+            uint32_t x[TKW_TILES][TK_KPL];
 #pragma unroll
-                for (int r = 0; r < TK_KPL / 4; ++r) {
-                    const uint4 q = *reinterpret_cast<const uint4 *>(keys + i0 + 4 * r);
-                    x[4 * r] = q.x;
-                    x[4 * r + 1] = q.y;
-                    x[4 * r + 2] = q.z;
-                    x[4 * r + 3] = q.w;
+            for (int q = 0; q < TKW_TILES; ++q) {
+                has[q] = todo != 0;  // wave-uniform
+                const int src = has[q] ? __builtin_ctzll(todo) : 0;
+                if (has[q]) todo &= todo - 1;
+                t[q] = tg + src;
+                const u64 i0 = t[q] * TK_TILE + (u64)lane * TK_KPL;
+                if (!has[q]) {
+#pragma unroll
+                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = 0u;
+                } else if (ALIGNED && t[q] * TK_TILE + TK_TILE <= n) {
+#pragma unroll
+                    for (int r = 0; r < TK_KPL / 4; ++r) {
+                        const uint4 v4 = *reinterpret_cast<const uint4 *>(keys + i0 + 4 * r);
+                        x[q][4 * r] = v4.x;
+                        x[q][4 * r + 1] = v4.y;
+                        x[q][4 * r + 2] = v4.z;
+                        x[q][4 * r + 3] = v4.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = i0 + j < n ? keys[i0 + j] : 0u;
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < TK_KPL; ++j) x[j] = i0 + j < n ? keys[i0 + j] : 0u;
             }
-            uint32_t mb = 0, me = 0;
 #pragma unroll
-            for (int j = 0; j < TK_KPL; ++j) {
-                const bool in = i0 + j < n;
-                const uint32_t u = key_of_i32(x[j]);
-                mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
-                me |= (uint32_t)(in && u == uv) << j;
-            }
-            const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
-            const uint32_t p = wave_incl_scan32(mine) - mine;
-            u64 b_before = bb + (p & 0xFFFFu);
-            u64 e_before = be + (p >> 16);
-            if (mb | me) {
+            for (int q = 0; q < TKW_TILES; ++q) {
+                if (!has[q]) break;  // wave-uniform
+                const int src = (int)(t[q] - tg);
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, src);
+                const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), src) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
+                const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
+                const u64 ce = tk_equal_of(c);
+                const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
+                const uint32_t total = tk_better_of(c) + (uint32_t)take_e;  // this tile's output keys
+                const u64 start = bb + (be < need ? be : need);            // and where they go
+                const u64 i0 = t[q] * TK_TILE + (u64)lane * TK_KPL;
+                uint32_t mb = 0, me = 0;
 #pragma unroll
                 for (int j = 0; j < TK_KPL; ++j) {
-                    u64 pos = ~0ull;
-                    if ((mb >> j) & 1) {
-                        pos = b_before + (e_before < need ? e_before : need);
-                        ++b_before;
-                    } else if ((me >> j) & 1) {
-                        if (e_before < need) pos = b_before + e_before;
-                        ++e_before;
-                    }
-                    if (pos != ~0ull) {
-                        const uint32_t r = (uint32_t)(pos - start);
-                        s_val[w][r] = x[j];
-                        s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                    const bool in = i0 + j < n;
+                    const uint32_t u = key_of_i32(x[q][j]);
+                    mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
+                    me |= (uint32_t)(in && u == uv) << j;
+                }
+                const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
+                const uint32_t p = wave_incl_scan32(mine) - mine;
+                u64 b_before = bb + (p & 0xFFFFu);
+                u64 e_before = be + (p >> 16);
+                if (mb | me) {
+#pragma unroll
+                    for (int j = 0; j < TK_KPL; ++j) {
+                        u64 pos = ~0ull;
+                        if ((mb >> j) & 1) {
+                            pos = b_before + (e_before < need ? e_before : need);
+                            ++b_before;
+                        } else if ((me >> j) & 1) {
+                            if (e_before < need) pos = b_before + e_before;
+                            ++e_before;
+                        }
+                        if (pos != ~0ull) {
+                            const uint32_t r = (uint32_t)(pos - start);
+                            s_val[w][r] = x[q][j];
+                            s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                        }
                     }
                 }
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
+                    if (vals) vals[start + r] = (int32_t)s_val[w][r];
+                    if (idx) idx[start + r] = (int64_t)(t[q] * TK_TILE + s_col[w][r]);
+                }
+                __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
             }
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
-                if (vals) vals[start + r] = (int32_t)s_val[w][r];
-                if (idx) idx[start + r] = (int64_t)(t * TK_TILE + s_col[w][r]);
-            }
-            __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
         }
     }
 }
