@@ -174,7 +174,7 @@ __device__ __forceinline__ void pick_pre(SelState &ss, const uint32_t *pre, uint
         const uint32_t b = threadIdx.x * PER + j;
         uint32_t sum = 0;
         if (b < nb)
-#pragma unroll 4
+#pragma unroll
             for (int c = 0; c < PRE_COPIES; ++c) sum += pre[c * PRE_BINS + b];
         h0[j] = sum;
     }
@@ -365,10 +365,10 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
 //     FIN_LDS_KEYS), every workgroup keeps its contiguous slice in LDS and the
 //     later digits scan LDS (each candidate level re-read the 21 MB of
 //     candidates: ~6 us a level at 2^30).
-//   * The first digit is 9 bits wide (FIN_D0; wider only when W > 30 needs
-//     it): every key of the domain lands in it, so every workgroup flushes
-//     nearly all of its bins -- 512 global atomics a workgroup into 4 copies,
-//     not 2048 onto one.  When k_main<0> has histogrammed it already
+//   * The first digit is 10 bits wide (FIN_D0; wider only when W > 32 would
+//     need it): every key of the domain lands in it, so every workgroup
+//     flushes nearly all of its bins -- 1024 global atomics a workgroup into 2
+//     copies, not 2048 onto one.  When k_main<0> has histogrammed it already
 //     (x.pre, PreHist: complete unless a workgroup flushed its staging
 //     mid-pass), it is picked from there: no histogram, flush or barrier.  The later digits only see the keys of one bin, and
 //     once that bin fits one workgroup's LDS, finish_tail ends the launch.

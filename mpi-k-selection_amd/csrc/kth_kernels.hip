@@ -77,19 +77,29 @@ struct StepArgs {
     uint32_t *pre_hist;    // k_main<0> (single-GPU window path): the candidates' first digit (PreHist), or null
 };
 
-// k_finish's first candidate digit: FIN_D0 bits ([257, 512] bins used: ~12-25 K
-// keys a bin from 6.3 M candidates at 2^30), wider only when W > 30 needs it
-constexpr uint32_t FIN_D0 = 9;
-__host__ __device__ __forceinline__ uint32_t fin_first_digit(uint32_t W) { return W > 30u ? W - 22u : FIN_D0; }
+// k_finish's first candidate digit: FIN_D0 bits ([513, 1024] bins used: ~6-12 K
+// keys a bin from 6.3 M candidates at 2^30 -- the tail's one workgroup then
+// resolves half the keys it did at 9 bits), wider only when W > 32 would need it
+#ifndef KTH_FIN_D0
+#define KTH_FIN_D0 10
+#endif
+constexpr uint32_t FIN_D0 = KTH_FIN_D0;
+__host__ __device__ __forceinline__ uint32_t fin_first_digit(uint32_t W) {
+    return W > FIN_D0 + 2u * DIGIT ? W - 2u * DIGIT : FIN_D0;  // (then two DIGIT-bit digits)
+}
 
 // The candidates' first digit, histogrammed by k_main<0> at the end of each
 // workgroup from its waves' staging regions (every candidate of a workgroup
 // is still there unless a wave had to flush its region mid-pass, which the
 // workgroup then reports in `incomplete` instead), into PRE_COPIES copies
-// (workgroup b adds to copy b % PRE_COPIES: 64 same-address adders a bin, not
-// 1024).  k_finish picks the digit from it without a histogram pass, a flush
+// (workgroup b adds to copy b % PRE_COPIES: 256 same-address adders a bin, not
+// 1024, and they finish over the pass's ~80 us of workgroup end times).  k_finish picks the digit from it without a histogram pass, a flush
 // or a grid barrier.  Two sets, alternate selects (k_finish clears the other).
-constexpr int PRE_COPIES = 16, PRE_BINS = 1024;  // a first digit of at most 10 bits (W <= 32)
+#ifndef KTH_PRE_COPIES
+#define KTH_PRE_COPIES 4
+#endif
+constexpr int PRE_COPIES = KTH_PRE_COPIES, PRE_BINS = 1024;  // a first digit of at most 10 bits (W <= 32)
+static_assert(FIN_D0 <= 10, "PreHist holds a first digit of at most 10 bits");
 constexpr int PRE_WORDS = PRE_COPIES * PRE_BINS + 64;  // u32: the copies, then `incomplete` (own 256-B line)
 constexpr int PRE_INCOMPLETE = PRE_COPIES * PRE_BINS;
 // the candidate domain of k_finish's decide(): v = key - (lo + 1) in [0, 2^W)

@@ -273,6 +273,14 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 #define KTH_TKW_TILES 2
 #endif
 constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
+#ifndef KTH_TKW_COAL
+#define KTH_TKW_COAL 0
+#endif
+constexpr bool TKW_COAL = KTH_TKW_COAL != 0;  // k_topk_write's tile layout (see there)
+// the column (key index within its tile) of lane l's key j
+__device__ __forceinline__ uint32_t tkw_col(int l, int j) {
+    return TKW_COAL ? (uint32_t)(256 * (j / 4) + 4 * l + (j & 3)) : (uint32_t)(l * TK_KPL + j);
+}
 template <bool ALIGNED, bool STAGED = false>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
@@ -305,7 +313,12 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
         u64 todo = __ballot(act);
         // TKW_TILES tiles a round: all their loads in flight together (one
         // tile's 4 KiB a wave left the loads idle while the tile was placed
-        // and copied out)
+        // and copied out: k = 2^27 1398 -> 1346 us on one box, ~equal on
+        // another).  Lane l owns keys 16 l .. 16 l + 15 (one wave scan a
+        // tile).  TKW_COAL=1: key 256 r + 4 l + j is component j of lane l's
+        // r-th 16-byte load (each load instruction reads 1 KiB contiguous)
+        // and the tile's order is row by row (four wave scans): measured no
+        // faster (1377 vs 1347 us at 2^27, 2339 vs 2322 at 2^29, same box).
         while (todo) {
             u64 t[TKW_TILES];
             bool has[TKW_TILES];
@@ -316,14 +329,15 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                 const int src = has[q] ? __builtin_ctzll(todo) : 0;
                 if (has[q]) todo &= todo - 1;
                 t[q] = tg + src;
-                const u64 i0 = t[q] * TK_TILE + (u64)lane * TK_KPL;
+                const u64 tb = t[q] * TK_TILE;
                 if (!has[q]) {
 #pragma unroll
                     for (int j = 0; j < TK_KPL; ++j) x[q][j] = 0u;
-                } else if (ALIGNED && t[q] * TK_TILE + TK_TILE <= n) {
+                } else if (ALIGNED && tb + TK_TILE <= n) {
 #pragma unroll
                     for (int r = 0; r < TK_KPL / 4; ++r) {
-                        const uint4 v4 = *reinterpret_cast<const uint4 *>(keys + i0 + 4 * r);
+                        const u64 o = TKW_COAL ? tb + 256 * r + 4 * lane : tb + (u64)lane * TK_KPL + 4 * r;
+                        const uint4 v4 = *reinterpret_cast<const uint4 *>(keys + o);
                         x[q][4 * r] = v4.x;
                         x[q][4 * r + 1] = v4.y;
                         x[q][4 * r + 2] = v4.z;
@@ -331,7 +345,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                     }
                 } else {
 #pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = i0 + j < n ? keys[i0 + j] : 0u;
+                    for (int j = 0; j < TK_KPL; ++j) {
+                        const u64 i = tb + tkw_col(lane, j);
+                        x[q][j] = i < n ? keys[i] : 0u;
+                    }
                 }
             }
 #pragma unroll
@@ -347,22 +364,20 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                 const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
                 const uint32_t total = tk_better_of(c) + (uint32_t)take_e;  // this tile's output keys
                 const u64 start = bb + (be < need ? be : need);            // and where they go
-                const u64 i0 = t[q] * TK_TILE + (u64)lane * TK_KPL;
-                uint32_t mb = 0, me = 0;
+                const u64 tb = t[q] * TK_TILE;
+                uint32_t mb = 0, me = 0;  // bit j: this lane's key j is better / equal
 #pragma unroll
                 for (int j = 0; j < TK_KPL; ++j) {
-                    const bool in = i0 + j < n;
+                    const bool in = tb + tkw_col(lane, j) < n;
                     const uint32_t u = key_of_i32(x[q][j]);
                     mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
                     me |= (uint32_t)(in && u == uv) << j;
                 }
-                const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
-                const uint32_t p = wave_incl_scan32(mine) - mine;
-                u64 b_before = bb + (p & 0xFFFFu);
-                u64 e_before = be + (p >> 16);
-                if (mb | me) {
-#pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) {
+                // place the kept keys of key group g (the lane's keys g * G .. g * G + G - 1, in
+                // the tile's order after the lanes before it): b_before / e_before count the
+                // group's better / equal keys before this lane's
+                auto place = [&](int g0, int G, u64 b_before, u64 e_before) {
+                    for (int j = g0; j < g0 + G; ++j) {
                         u64 pos = ~0ull;
                         if ((mb >> j) & 1) {
                             pos = b_before + (e_before < need ? e_before : need);
@@ -374,14 +389,31 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                         if (pos != ~0ull) {
                             const uint32_t r = (uint32_t)(pos - start);
                             s_val[w][r] = x[q][j];
-                            s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                            s_col[w][r] = (uint16_t)tkw_col(lane, j);
                         }
                     }
+                };
+                if constexpr (TKW_COAL) {
+                    u64 b_run = bb, e_run = be;  // the rows before this one
+#pragma unroll
+                    for (int r = 0; r < TK_KPL / 4; ++r) {
+                        const uint32_t mine = (uint32_t)__popc((mb >> (4 * r)) & 0xFu) |
+                                              ((uint32_t)__popc((me >> (4 * r)) & 0xFu) << 16);
+                        const uint32_t incl = wave_incl_scan32(mine), p = incl - mine;
+                        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+                        if (((mb | me) >> (4 * r)) & 0xFu) place(4 * r, 4, b_run + (p & 0xFFFFu), e_run + (p >> 16));
+                        b_run += tot & 0xFFFFu;
+                        e_run += tot >> 16;
+                    }
+                } else {
+                    const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
+                    const uint32_t p = wave_incl_scan32(mine) - mine;
+                    if (mb | me) place(0, TK_KPL, bb + (p & 0xFFFFu), be + (p >> 16));
                 }
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
                     if (vals) vals[start + r] = (int32_t)s_val[w][r];
-                    if (idx) idx[start + r] = (int64_t)(t[q] * TK_TILE + s_col[w][r]);
+                    if (idx) idx[start + r] = (int64_t)(tb + s_col[w][r]);
                 }
                 __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
             }
