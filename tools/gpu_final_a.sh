@@ -1,4 +1,4 @@
-# Round 4 evidence (a): the whole GPU suite, smoke(), the default bench line
+# Evidence (a): the whole GPU suite, smoke(), the default bench line
 # (the driver's N=1 command, with CPU baselines) and its rocprof kernel stats.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/fa; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
@@ -36,8 +36,8 @@ for l in open('$O/adv.jsonl'):
     d=json.loads(l); c=d['config']
     print(c.get('family', '?'), 'k', c.get('k'), round(d['value'],1), 'Gkeys/s', round(d['ms_per_step'],4), 'ms', 'path', d.get('path'), 'cands', d.get('candidates'), d['verified'])"
 echo "== rows (BASELINE config 5: uniform and duplicate-heavy, k-th and top-k)"
-for args in "--rows-dtype i32" "--rows-dtype f32" "--rows-dtype i32 --topk" "--rows-dtype f32 --topk" "--rows-dtype i32 --rows-input dup" "--rows-dtype f32 --rows-input dup"; do
-  timeout -k 10 120 python -u bench.py --workload rows $args --k 64 --steps 20 --warmup 3 >> $O/rows.jsonl 2>$O/rows.err || { echo "rows $args rc=$?"; tail -20 $O/rows.err; exit 1; }
+for args in "--rows-dtype i32" "--rows-dtype f32" "--rows-dtype i32 --topk" "--rows-dtype f32 --topk" "--rows-dtype i32 --rows-input dup" "--rows-dtype f32 --rows-input dup" "--rows-dtype f32 --rows-input dup --k 2048"; do
+  timeout -k 10 120 python -u bench.py --workload rows --k 64 $args --steps 20 --warmup 3 >> $O/rows.jsonl 2>$O/rows.err || { echo "rows $args rc=$?"; tail -20 $O/rows.err; exit 1; }
 done
 python3 -c "
 import json

@@ -1,4 +1,4 @@
-# Round 4 evidence (b): PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE
+# Evidence (b): PMC HBM traffic (separate FETCH_SIZE / WRITE_SIZE
 # passes) on the final build for the select, the rows (k-th and top-k) and the
 # staged top-k; the 2^33 lines; the SQ instruction mix of k_main and the rows
 # kernels.
@@ -24,7 +24,7 @@ for dt in i32 f32; do
   pmc2 rows_topk_$dt -- --workload rows --rows-dtype $dt --topk --k 64 --steps 3 --warmup 1
   python3 tools/pmc_traffic.py $(csv rows_topk_$dt FETCH_SIZE) $(csv rows_topk_$dt WRITE_SIZE) rows_reg 28 rows_topk_$dt $O/pmc_traffic_rows_topk_$dt.json 33554432 | tail -4
 done
-for k in 1048576 67108864; do
+for k in 1048576 67108864 134217728 536870912; do
   echo "== PMC top-k k=$k"
   pmc2 topk_$k -- --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline
   python3 tools/pmc_topk.py $(csv topk_$k FETCH_SIZE) $(csv topk_$k WRITE_SIZE) 30 uniform_half $k $O/pmc_traffic_topk_k$k.json

@@ -1,6 +1,6 @@
-# Round 4: rocprof kernel stats of the config-5 workloads and two top-k calls on the final build
+# rocprof kernel stats of the config-5 workloads and two top-k calls on the final build
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r4rp; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/rowsprof; rm -rf $O; mkdir -p $O; export TMPDIR=/tmp
 i=0
 for args in "--workload rows --rows-dtype i32 --k 64" "--workload rows --rows-dtype f32 --k 64" "--workload rows --rows-dtype i32 --topk --k 64" "--workload rows --rows-dtype f32 --topk --k 64" "--workload rows --rows-dtype i32 --rows-input dup --k 64" "--workload rows --rows-dtype f32 --rows-input dup --k 64" "--workload topk --k 1048576" "--workload topk --k 67108864"; do
   i=$((i+1))
