@@ -23,16 +23,6 @@
 
 namespace kth {
 
-constexpr int HEAD_LEVELS = 3;       // sample digits: 11 + 11 + 10 bits
-constexpr int FIN_LEVELS = 3;        // candidate / input digits
-constexpr int HEAD_UNROLL = 4;       // 16-B loads per thread per sample tile (16 Ki keys per 1024-thread tile)
-constexpr int BAR_GROUP_STRIDE = 64; // words between group counters (separate 256-B lines)
-constexpr int BAR_BASE = 8 * BAR_GROUP_STRIDE, BAR_ERR = BAR_BASE + BAR_GROUP_STRIDE;
-constexpr int BAR_TAIL = BAR_ERR + BAR_GROUP_STRIDE;  // u64 at this u32 index: k_finish tail (arrivals << 32 | keys)
-constexpr int BAR_WORDS = BAR_TAIL + BAR_GROUP_STRIDE;  // u32 words of barrier state per ctx
-constexpr uint32_t BAR_SPIN_LIMIT = 1u << 21;         // polls before a barrier gives up (seconds)
-constexpr uint32_t ERR_BARRIER = 64;
-
 struct CoopArgs {
     u64 *slots;        // HEAD_LEVELS / FIN_LEVELS histogram slots of STATS_WORDS, zero on entry
     uint32_t *bar;     // BAR_WORDS of barrier state
@@ -47,95 +37,6 @@ struct CoopArgs {
     const uint32_t *pre;  // k_finish: k_main<0>'s first candidate digit (PreHist), or null
     uint32_t *pre_zero;   // k_finish: the other PreHist set, cleared for the next select
 };
-
-// This wave's outstanding global accesses (atomics, write-through stores) are
-// performed: every wave of a workgroup waits before its barrier arrival.
-__device__ __forceinline__ void wait_mem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Grid-wide barrier of the calling kernel (all threads call).  Data crosses
-// workgroups inside these kernels only through device-coherent accesses --
-// histogram atomics, write-through (sc1) stores, sc1 loads -- so the barrier
-// needs no L2 write-back / invalidate (an agent-scope release / acquire fence
-// per workgroup made every barrier ~10 us: 32 workgroups per XCD each
-// flushing and invalidating the shared L2).  Each wave waits for its own
-// accesses to be performed before the workgroup arrives.
-//
-// Arrival is one non-returning atomic add on the workgroup's group counter
-// (blockIdx % 8: same-address atomics serialise, ~36 ns each); lanes 0..7 of
-// wave 0 then poll all group counters at once until each has reached its
-// target.  Counters only grow (u32, compared modulo 2^32): the value a group
-// counter had when the kernel started is kept in bar[BAR_BASE + g], written
-// by workgroup 0 of the previous barrier kernel at its end (GridBar::finish),
-// so no reset, no last-arriver hand-off and nothing zeroed between calls --
-// two memory round trips on the critical path.  Every spin is bounded: a
-// barrier that does not complete raises bar[BAR_ERR] and returns ok = false.
-struct GridBar {
-    uint32_t *bar;
-    uint32_t n;  // barriers passed in this kernel
-};
-
-__device__ __forceinline__ uint32_t group_size(uint32_t g) { return (gridDim.x - g + 7u) / 8u; }
-
-// Kernel start: every thread calls; s_base is LDS of 8 words.
-__device__ __forceinline__ GridBar grid_bar_init(uint32_t *bar, uint32_t *s_base) {
-    if (threadIdx.x < 8) s_base[threadIdx.x] = bar[BAR_BASE + threadIdx.x];
-    return GridBar{bar, 0u};
-}
-
-__device__ __forceinline__ void grid_sync(GridBar &gb, const uint32_t *s_base, bool &ok) {
-    __shared__ uint32_t s_ok;
-    wait_mem();
-    __syncthreads();
-    gb.n++;
-    if (threadIdx.x < WAVE) {
-        const uint32_t lane = threadIdx.x, groups = gridDim.x < 8u ? gridDim.x : 8u;
-        if (lane == 0)
-            __hip_atomic_fetch_add(gb.bar + (blockIdx.x & 7u) * BAR_GROUP_STRIDE, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t target = lane < groups ? s_base[lane] + gb.n * group_size(lane) : 0u;
-        bool done = lane >= groups;
-        uint32_t spins = 0, good = 1;
-        while (true) {
-            if (!done) {
-                const uint32_t v = __hip_atomic_load(gb.bar + lane * BAR_GROUP_STRIDE, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                done = (int32_t)(v - target) >= 0;
-            }
-            if (__ballot(!done) == 0) break;  // wave-uniform
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins >= BAR_SPIN_LIMIT) {
-                good = 0;
-                if (lane == 0) __hip_atomic_fetch_or(gb.bar + BAR_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        if (lane == 0) s_ok = good;
-    }
-    __syncthreads();
-    ok = ok && s_ok != 0;
-}
-
-// Kernel end, workgroup 0 (after its last barrier): the counters' values for
-// the next barrier kernel.  Every workgroup passes the same number of barriers.
-__device__ __forceinline__ void grid_bar_finish(const GridBar &gb, const uint32_t *s_base) {
-    if (blockIdx.x == 0 && threadIdx.x < 8) gb.bar[BAR_BASE + threadIdx.x] = s_base[threadIdx.x] + gb.n * group_size(threadIdx.x);
-}
-
-// Load a level's reduced histograms (thread i: bins [i*PER, i*PER + PER)) with
-// device-coherent loads, and pick.
-template <int BLOCK>
-__device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool share, u64 *scratch,
-                                          const EarlyWindow *ew, u64 *cnt0 = nullptr) {
-    constexpr int PER = NBINS / BLOCK;
-    u64 h0[PER], h1[PER];
-    const u64 *b0 = slot + NCOUNTS + threadIdx.x * PER;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        h0[j] = __hip_atomic_load(b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h1[j] = share ? 0ull : __hip_atomic_load(b0 + NBINS + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    pick_state<BLOCK, PER>(ss, h0, h1, share, scratch, ew, cnt0);
-}
 
 // The dense first digit of k_finish (nb <= NBINS / copies bins) is flushed
 // into `copies` histogram copies (workgroup w adds to copy w % copies: fewer
@@ -192,70 +93,6 @@ __device__ __forceinline__ void hist_flush_copies(uint32_t (*lh)[NBINS], uint32_
     }
 }
 
-// Device-coherent (sc1) 16-byte loads of a buffer other workgroups of this
-// kernel wrote with write-through stores (k_head's sample).
-struct CoherentBuf {
-    __amdgpu_buffer_rsrc_t r;
-    __device__ CoherentBuf(const void *p, uint32_t bytes)
-        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000)) {}
-    __device__ __forceinline__ uint4 load16(uint32_t byte_off) const {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16 /* sc1 */);
-        return make_uint4(v[0], v[1], v[2], v[3]);
-    }
-};
-
-// k_head's gather of the full 1024-key sample chunks: the first digit of a
-// fresh selection has one histogram (both window targets share the empty
-// prefix) and no prefix test, so a key costs a shift and one LDS atomic; the
-// chunk is written through as 16-byte stores (per-key 4-byte atomic stores and
-// bounds tests made the gather ~8 us of VALU issue in 64 CUs).  Chunk c of the
-// sample = keys[c * stride, + SAMPLE_CHUNK); lane l holds 16-byte words l, l+64,
-// l+128, l+192 of it.  Returns false (nothing done) unless every chunk is full
-// and 16-byte aligned; the caller then uses gather_chunks.
-template <int BLOCK>
-__device__ __forceinline__ bool gather_head_fast(const int32_t *__restrict__ keys, u64 stride, uint32_t *sample,
-                                                 u64 s, uint32_t (*lh)[NBINS], const HistPlan &plan) {
-    static_assert(SAMPLE_CK == 16, "four 16-byte words per lane and chunk");
-    // (selects, not plan.x[t]: a runtime index made the plan a private array
-    // that the compiler moved into 44 KiB of LDS)
-    const bool one = plan.h[0] != plan.h[1];  // exactly one histogram
-    const bool t1 = !plan.h[0];
-    if (s % SAMPLE_CHUNK != 0 || (reinterpret_cast<uintptr_t>(keys) & 15u) != 0 || stride % 4 != 0 || !one ||
-        (t1 ? plan.done[1] : plan.done[0]) != 0 || plan.base != 0u)
-        return false;
-    const uint32_t sh = t1 ? plan.shift[1] : plan.shift[0], mask = t1 ? plan.mask[1] : plan.mask[0];
-    uint32_t *h = t1 ? lh[1] : lh[0];
-    const __amdgpu_buffer_rsrc_t out =
-        __builtin_amdgcn_make_buffer_rsrc(sample, (short)0, (int)(s * 4), 0x00020000);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const u64 nchunks = s / SAMPLE_CHUNK;
-    const u64 gw = ((u64)blockIdx.x * BLOCK + threadIdx.x) / WAVE, nw = (u64)gridDim.x * (BLOCK / WAVE);
-    for (u64 c = gw; c < nchunks; c += nw) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
-        uint4 q[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            q[r].x ^= 0x80000000u;
-            q[r].y ^= 0x80000000u;
-            q[r].z ^= 0x80000000u;
-            q[r].w ^= 0x80000000u;
-            u32x4 v = {q[r].x, q[r].y, q[r].z, q[r].w};
-            __builtin_amdgcn_raw_buffer_store_b128(v, out, (int)((c * SAMPLE_CHUNK + 4 * (r * WAVE + lane)) * 4), 0,
-                                                   16 /* sc1: written through */);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            atomicAdd(&h[(q[r].x >> sh) & mask], 1u);
-            atomicAdd(&h[(q[r].y >> sh) & mask], 1u);
-            atomicAdd(&h[(q[r].z >> sh) & mask], 1u);
-            atomicAdd(&h[(q[r].w >> sh) & mask], 1u);
-        }
-    }
-    return true;
-}
-
 __device__ __forceinline__ uint32_t active_wgs(u64 count, u64 per_wg) {
     const u64 want = (count + per_wg - 1) / per_wg;
     return (uint32_t)(want < (u64)gridDim.x ? want : (u64)gridDim.x);
@@ -272,7 +109,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
     __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
-    __shared__ uint32_t s_base[8];
+    __shared__ uint32_t s_base[BAR_NG];
     KTH_STAMP(a, 0);
     GridBar gb = grid_bar_init(x.bar, s_base);
     for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
@@ -302,9 +139,17 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
             }
         }
     };
-    if (x.sample_ready)  // block-uniform
+    bool from_chunks = false;  // block-uniform (kernel arguments and the fresh state)
+#ifdef KTH_HEAD_STORE_SAMPLE  // design exploration: the round-4 head (sample written through)
+    constexpr bool kHeadStore = true;
+#else
+    constexpr bool kHeadStore = false;
+#endif
+    if (x.sample_ready)
         hist_sample();
-    else if (!gather_head_fast<DENSE_BLK>(keys, stride, sample, s, lh, plan))
+    else if (gather_head_fast<DENSE_BLK, kHeadStore>(keys, stride, sample, s, lh, plan, blockIdx.x, gridDim.x))
+        from_chunks = !kHeadStore;
+    else
         gather_chunks<DENSE_BLK, true, true>(keys, n_keys, stride, sample, s, lh, plan);
 #ifdef KTH_HEAD_DIAG  // diagnostic build: gather / flush / drain times (slots 4-6 are free on an early window)
     KTH_STAMP(a, 4);
@@ -330,7 +175,11 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
         for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK)
             reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        hist_sample();
+        if (from_chunks)  // (the fast gather keeps no sample: writing 4 MiB through and waiting
+                          // for it before the barrier cost more than re-reading the chunks)
+            head_hist_chunks<DENSE_BLK>(keys, stride, s, lh, plan, blockIdx.x, gridDim.x);
+        else
+            hist_sample();
         hist_flush<DENSE_BLK>(lh, plan, x.slots + (size_t)(L + 1) * STATS_WORDS);
         if (L == 0) KTH_STAMP(a, 4);
     }
@@ -605,7 +454,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_finish(StepArgs a, CoopArgs x) {
     __shared__ u64 scratch[2 * (DENSE_BLK / WAVE) + 8];
     __shared__ __attribute__((aligned(16))) uint32_t lh[2][NBINS];
     extern __shared__ uint4 res[];  // FIN_LDS_KEYS / 4 entries (dynamic)
-    __shared__ uint32_t s_base[8];
+    __shared__ uint32_t s_base[BAR_NG];
     __shared__ u64 s_cnt0;
     KTH_STAMP(a, 0);
     GridBar gb = grid_bar_init(x.bar, s_base);

@@ -19,6 +19,7 @@
 #include <type_traits>
 
 #include "kth_device.hpp"
+#include "kth_gridbar.hpp"
 
 namespace kth {
 
@@ -590,6 +591,104 @@ __global__ __launch_bounds__(DENSE_BLK) void k_gather(StepArgs a, const int32_t 
     KTH_STAMP(a, 5);
 }
 
+// Load a level's reduced histograms (thread i: bins [i*PER, i*PER + PER)) with
+// device-coherent loads, and pick.
+template <int BLOCK>
+__device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool share, u64 *scratch,
+                                          const EarlyWindow *ew, u64 *cnt0 = nullptr) {
+    constexpr int PER = NBINS / BLOCK;
+    u64 h0[PER], h1[PER];
+    const u64 *b0 = slot + NCOUNTS + threadIdx.x * PER;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        h0[j] = __hip_atomic_load(b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h1[j] = share ? 0ull : __hip_atomic_load(b0 + NBINS + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    pick_state<BLOCK, PER>(ss, h0, h1, share, scratch, ew, cnt0);
+}
+
+// k_head's gather of the full 1024-key sample chunks: the first digit of a
+// fresh selection has one histogram (both window targets share the empty
+// prefix) and no prefix test, so a key costs a shift and one LDS atomic; the
+// chunk is written through as 16-byte stores (per-key 4-byte atomic stores and
+// bounds tests made the gather ~8 us of VALU issue in 64 CUs).  Chunk c of the
+// sample = keys[c * stride, + SAMPLE_CHUNK); lane l holds 16-byte words l, l+64,
+// l+128, l+192 of it.  Returns false (nothing done) unless every chunk is full
+// and 16-byte aligned; the caller then uses gather_chunks.
+// STORE = false: the chunk's keys only go into the histogram (the sample is
+// not kept: a later sample level re-reads the chunks from the input).
+// wg / nwg: this workgroup among the nwg that share the chunks.
+template <int BLOCK, bool STORE = true>
+__device__ __forceinline__ bool gather_head_fast(const int32_t *__restrict__ keys, u64 stride, uint32_t *sample,
+                                                 u64 s, uint32_t (*lh)[NBINS], const HistPlan &plan,
+                                                 uint32_t wg, uint32_t nwg) {
+    static_assert(SAMPLE_CK == 16, "four 16-byte words per lane and chunk");
+    // (selects, not plan.x[t]: a runtime index made the plan a private array
+    // that the compiler moved into 44 KiB of LDS)
+    const bool one = plan.h[0] != plan.h[1];  // exactly one histogram
+    const bool t1 = !plan.h[0];
+    if (s % SAMPLE_CHUNK != 0 || (reinterpret_cast<uintptr_t>(keys) & 15u) != 0 || stride % 4 != 0 || !one ||
+        (t1 ? plan.done[1] : plan.done[0]) != 0 || plan.base != 0u)
+        return false;
+    const uint32_t sh = t1 ? plan.shift[1] : plan.shift[0], mask = t1 ? plan.mask[1] : plan.mask[0];
+    uint32_t *h = t1 ? lh[1] : lh[0];
+    const __amdgpu_buffer_rsrc_t out =
+        __builtin_amdgcn_make_buffer_rsrc(sample, (short)0, (int)(s * 4), 0x00020000);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const u64 nchunks = s / SAMPLE_CHUNK;
+    const u64 gw = ((u64)wg * BLOCK + threadIdx.x) / WAVE, nw = (u64)nwg * (BLOCK / WAVE);
+    for (u64 c = gw; c < nchunks; c += nw) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
+        uint4 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            q[r].x ^= 0x80000000u;
+            q[r].y ^= 0x80000000u;
+            q[r].z ^= 0x80000000u;
+            q[r].w ^= 0x80000000u;
+            if (STORE) {
+                u32x4 v = {q[r].x, q[r].y, q[r].z, q[r].w};
+                __builtin_amdgcn_raw_buffer_store_b128(v, out, (int)((c * SAMPLE_CHUNK + 4 * (r * WAVE + lane)) * 4),
+                                                       0, 16 /* sc1: written through */);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            atomicAdd(&h[(q[r].x >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].y >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].z >> sh) & mask], 1u);
+            atomicAdd(&h[(q[r].w >> sh) & mask], 1u);
+        }
+    }
+    return true;
+}
+
+// A later sample digit over the full 1024-key chunks of the input themselves
+// (the fast gather keeps no sample): workgroup wg of nwg, plan's histograms.
+template <int BLOCK>
+__device__ __forceinline__ void head_hist_chunks(const int32_t *__restrict__ keys, u64 stride, u64 s,
+                                                 uint32_t (*lh)[NBINS], const HistPlan &plan, uint32_t wg,
+                                                 uint32_t nwg) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const u64 nchunks = s / SAMPLE_CHUNK;
+    const u64 gw = ((u64)wg * BLOCK + threadIdx.x) / WAVE, nw = (u64)nwg * (BLOCK / WAVE);
+    for (u64 c = gw; c < nchunks; c += nw) {  // wave-convergent
+        const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
+        uint4 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            hist_add<BLOCK>(lh, plan, q[r].x ^ 0x80000000u, true);
+            hist_add<BLOCK>(lh, plan, q[r].y ^ 0x80000000u, true);
+            hist_add<BLOCK>(lh, plan, q[r].z ^ 0x80000000u, true);
+            hist_add<BLOCK>(lh, plan, q[r].w ^ 0x80000000u, true);
+        }
+    }
+}
+
 // The streaming pass.  Window [lo, hi] comes from the advance (last sample
 // digit).  Per key: #<lo, #==lo, #==hi in per-lane registers.  Keys strictly
 // inside the window are staged in the wave's private LDS region one key slot
@@ -1027,7 +1126,9 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         // the next tile's first 1 / 2 / 4 loads issued before this tile is used
         // 0.703 / 0.695 / 0.689.  The top-k variants' own schedule sent all
         // eight first: k_main<5> ~750 us.  Fewer requests in flight per wave
-        // at a tile's start stream faster here, not more.
+        // at a tile's start stream faster here, not more.  Plain loads instead
+        // of nontemporal ones: select 0.676 -> 0.762 ms, top-k k = 2^24 / 2^27
+        // 1.003 / 2.015 -> 1.082 / 2.126 ms (one box, round 5).
 #ifndef KTH_MAIN_FIRST  // design exploration: loads before the wait, and the wait's vmcnt
 #define KTH_MAIN_FIRST 1
 #define KTH_MAIN_WAITN 0

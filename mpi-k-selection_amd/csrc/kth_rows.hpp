@@ -449,14 +449,18 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
             amax = max(amax, end_key(vhi));
         }
         if (vlo == 0.f || vhi == 0.f) {  // wave-uniform
-            uint32_t nz = 0, pz = 0;  // this lane's -0.0 / +0.0 keys
+            // the row's -0.0 / +0.0 counts: one compare a key, counted on the
+            // scalar unit (ballot + popcount, no wave sum); a bin of zeros
+            // only (vlo == vhi == 0) holds all of them: +0.0 = cnt - (-0.0)
+            uint32_t cn = 0, cp = 0;
 #pragma unroll
-            for (int j = 0; j < KPL; ++j) {
-                nz += key[j] == 0x80000000u ? 1u : 0u;
-                pz += key[j] == 0u ? 1u : 0u;
+            for (int j = 0; j < KPL; ++j) cn += (uint32_t)__popcll(__ballot(key[j] == 0x80000000u));
+            if (vlo == 0.f && vhi == 0.f) {  // wave-uniform
+                cp = cnt - cn;
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPL; ++j) cp += (uint32_t)__popcll(__ballot(key[j] == 0u));
             }
-            const auto add = [](uint32_t a, uint32_t b) { return a + b; };
-            const uint32_t cn = wave_reduce(nz, 0u, add), cp = wave_reduce(pz, 0u, add);
             const uint32_t kn = end_key(-0.0f), kp = end_key(0.0f);
             if (cn) {
                 amin = min(amin, kn);

@@ -165,7 +165,24 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
 // Pass 0 (META, before k_topk_count, into zeroed counts): the candidates'
 // share of their rows' counts, one atomic per candidate better than or equal
 // to v (no read: a row k_topk_count then counts from the input is simply
-// overwritten there; rows past ncov carry row ~0u).
+// overwritten there; rows past ncov carry row ~0u).  A wave takes TKC_U x 64
+// consecutive candidates, lane l every 64th, with all their loads in flight
+// (one candidate a lane waited a memory round trip per 64: 48 us at k = 2^27);
+// each atomic instruction then covers 64 consecutive candidates, whose rows
+// (~6 candidates a row at 2^30) share a few cache lines of the counts.  (Runs
+// of 8 consecutive candidates per lane, one atomic per run of equal rows:
+// fewer atomics, but each instruction's spread over ~64 lines: 68 us.)
+// TKC_SEG: one atomic per run of equal rows among a wave-instruction's 64
+// (k = 2^27 / 2^29: 34 / 42 us against 50 / 105 for one per candidate, and
+// 48 / 102 with one candidate a lane).
+#ifndef KTH_TKC_U
+#define KTH_TKC_U 8
+#endif
+constexpr int TKC_U = KTH_TKC_U;  // candidates a lane loads together
+#ifndef KTH_TKC_SEG
+#define KTH_TKC_SEG 1
+#endif
+constexpr bool TKC_SEG = KTH_TKC_SEG != 0;  // one atomic per run of equal rows in a wave (see there)
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restrict__ cand,
                                                          const uint32_t *__restrict__ rows,
                                                          const u64 *__restrict__ cand_count, u64 cap,
@@ -176,14 +193,42 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restr
     if (!tk_meta_ok(tflags, d_v, st)) return;
     const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const u64 m = min(*cand_count, cap);
-    for (u64 i = (u64)blockIdx.x * TK_BLOCK + threadIdx.x; i < m; i += (u64)gridDim.x * TK_BLOCK) {
-        const uint32_t r = rows[i];
-        if (r == ~0u) continue;  // outside k_main's rows (counted from the input)
-        const uint32_t u = cand[i];
-        if (tk_better(u, uv, flip))
-            atomicAdd(&tcnt[r], 1u);
-        else if (u == uv)
-            atomicAdd(&tcnt[r], 0x10000u);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
+    for (u64 b = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + threadIdx.x / WAVE) * (TKC_U * WAVE); b < m;
+         b += nw * (TKC_U * WAVE)) {
+        uint32_t u[TKC_U], r[TKC_U];
+#pragma unroll
+        for (int q = 0; q < TKC_U; ++q) {
+            const u64 i = b + (u64)q * WAVE + lane;
+            r[q] = i < m ? rows[i] : ~0u;
+            u[q] = i < m ? cand[i] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < TKC_U; ++q) {
+            const uint32_t c = tk_better(u[q], uv, flip) ? 1u : (u[q] == uv ? 0x10000u : 0u);
+            if (TKC_SEG) {
+                // one atomic per run of equal rows among the wave's 64: the
+                // run's last lane adds (prefix sum here) - (prefix sum at the
+                // run before); prefix sums never decrease (fields <= 64), so
+                // "at the run before" is a max-scan of the runs' last lanes
+                const uint32_t rn = (uint32_t)__shfl_down((int)r[q], 1, WAVE);
+                const bool last = lane == WAVE - 1 || rn != r[q];
+                const uint32_t S = wave_incl_scan32(c);
+                uint32_t T = last ? S : 0u;
+                T = max(T, dpp32<0x111, 0xF>(T));
+                T = max(T, dpp32<0x112, 0xF>(T));
+                T = max(T, dpp32<0x114, 0xF>(T));
+                T = max(T, dpp32<0x118, 0xF>(T));
+                T = max(T, dpp32<0x142, 0xA>(T));
+                T = max(T, dpp32<0x143, 0xC>(T));
+                const uint32_t before = (uint32_t)__shfl_up((int)T, 1, WAVE);
+                const uint32_t add = S - (lane == 0 ? 0u : before);
+                if (last && r[q] != ~0u && add) atomicAdd(&tcnt[r[q]], add);
+            } else if (r[q] != ~0u && c) {  // (~0u: past m, or outside k_main's rows: counted from the input)
+                atomicAdd(&tcnt[r[q]], c);
+            }
+        }
     }
 }
 
@@ -267,20 +312,20 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 // lane) and visits only those holding output keys.  Lane l owns keys
 // [1024 t + 16 l, +16) of tile t, so a wave scan of the per-lane counts gives
 // every kept key its slot in the tile's output range, which is contiguous:
-// [bb + min(be, need), + #better + #kept ties).  The pairs are staged in the
-// wave's LDS and written out coalesced.
+// [bb + min(be, need), + #better + #kept ties).  Inside the range a key's
+// slot is 32-bit arithmetic: with pb / pe the better / equal keys of the tile
+// before it and cap = clamp(need - be, 0, 65535) the ties the tile may still
+// take, a better key goes to pb + min(pe, cap), a tie with pe < cap to pb + pe.
+// The pairs are staged in the wave's LDS and written out coalesced.
+// Measured (rocprof averages, k = 2^27 / 2^29): nontemporal key loads 1436 /
+// 2336 us against plain loads 1251 / 1934 (one box); four tiles a round
+// against two 1261 / 2251 against 1304 / 2275 (another box).  Also measured
+// and dropped there: nontemporal output stores (1433 / 2952) and issuing the
+// next round's loads before placing this one (142 VGPRs; 1284 / 2279).
 #ifndef KTH_TKW_TILES
-#define KTH_TKW_TILES 2
+#define KTH_TKW_TILES 4
 #endif
 constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
-#ifndef KTH_TKW_COAL
-#define KTH_TKW_COAL 0
-#endif
-constexpr bool TKW_COAL = KTH_TKW_COAL != 0;  // k_topk_write's tile layout (see there)
-// the column (key index within its tile) of lane l's key j
-__device__ __forceinline__ uint32_t tkw_col(int l, int j) {
-    return TKW_COAL ? (uint32_t)(256 * (j / 4) + 4 * l + (j & 3)) : (uint32_t)(l * TK_KPL + j);
-}
 template <bool ALIGNED, bool STAGED = false>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
@@ -297,6 +342,40 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
     const u64 t_from = STAGED && tk5_ok(tflags, d_v) ? ncov : 0;  // tiles below t_from: k_tk5_write
+    // one round: up to TKW_TILES tiles of the wave's 64 (the next set bits of todo)
+    struct Round {
+        int src[TKW_TILES];  // lane (tile - tg) of each tile, -1 past the last
+        uint32_t x[TKW_TILES][TK_KPL];
+    };
+    auto load_round = [&](Round &rd, u64 &todo, u64 tg) {
+#pragma unroll
+        for (int q = 0; q < TKW_TILES; ++q) {
+            const bool has = todo != 0;  // wave-uniform
+            rd.src[q] = has ? __builtin_ctzll(todo) : -1;
+            if (has) todo &= todo - 1;
+            const u64 tb = (tg + (u64)(has ? rd.src[q] : 0)) * TK_TILE;
+            if (!has) {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) rd.x[q][j] = 0u;
+            } else if (ALIGNED && tb + TK_TILE <= n) {
+#pragma unroll
+                for (int r = 0; r < TK_KPL / 4; ++r) {
+                    const uint4 *p4 = reinterpret_cast<const uint4 *>(keys + tb + (u64)lane * TK_KPL + 4 * r);
+                    const uint4 v4 = *p4;
+                    rd.x[q][4 * r] = v4.x;
+                    rd.x[q][4 * r + 1] = v4.y;
+                    rd.x[q][4 * r + 2] = v4.z;
+                    rd.x[q][4 * r + 3] = v4.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) {
+                    const u64 i = tb + (u64)lane * TK_KPL + j;
+                    rd.x[q][j] = i < n ? keys[i] : 0u;
+                }
+            }
+        }
+    };
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + w) * WAVE; tg < ntiles; tg += nw * WAVE) {
         if (tg + WAVE <= t_from) continue;  // wave-uniform
         // lane l: tile tg + l's bases and whether it holds output keys
@@ -311,104 +390,53 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
         }
         const bool act = tl >= t_from && (tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need));
         u64 todo = __ballot(act);
-        // TKW_TILES tiles a round: all their loads in flight together (one
+        // TKW_TILES tiles a round, all their loads in flight together (one
         // tile's 4 KiB a wave left the loads idle while the tile was placed
         // and copied out: k = 2^27 1398 -> 1346 us on one box, ~equal on
-        // another).  Lane l owns keys 16 l .. 16 l + 15 (one wave scan a
-        // tile).  TKW_COAL=1: key 256 r + 4 l + j is component j of lane l's
-        // r-th 16-byte load (each load instruction reads 1 KiB contiguous)
-        // and the tile's order is row by row (four wave scans): measured no
-        // faster (1377 vs 1347 us at 2^27, 2339 vs 2322 at 2^29, same box).
+        // another).  (A layout in which each load instruction reads 1 KiB
+        // contiguous, four wave scans a tile, measured no faster: 1377 vs
+        // 1347 us at 2^27, 2339 vs 2322 at 2^29.)
         while (todo) {
-            u64 t[TKW_TILES];
-            bool has[TKW_TILES];
-            uint32_t x[TKW_TILES][TK_KPL];
+            Round cur;
+            load_round(cur, todo, tg);
 #pragma unroll
             for (int q = 0; q < TKW_TILES; ++q) {
-                has[q] = todo != 0;  // wave-uniform
-                const int src = has[q] ? __builtin_ctzll(todo) : 0;
-                if (has[q]) todo &= todo - 1;
-                t[q] = tg + src;
-                const u64 tb = t[q] * TK_TILE;
-                if (!has[q]) {
-#pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = 0u;
-                } else if (ALIGNED && tb + TK_TILE <= n) {
-#pragma unroll
-                    for (int r = 0; r < TK_KPL / 4; ++r) {
-                        const u64 o = TKW_COAL ? tb + 256 * r + 4 * lane : tb + (u64)lane * TK_KPL + 4 * r;
-                        const uint4 v4 = *reinterpret_cast<const uint4 *>(keys + o);
-                        x[q][4 * r] = v4.x;
-                        x[q][4 * r + 1] = v4.y;
-                        x[q][4 * r + 2] = v4.z;
-                        x[q][4 * r + 3] = v4.w;
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) {
-                        const u64 i = tb + tkw_col(lane, j);
-                        x[q][j] = i < n ? keys[i] : 0u;
-                    }
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < TKW_TILES; ++q) {
-                if (!has[q]) break;  // wave-uniform
-                const int src = (int)(t[q] - tg);
+                const int src = cur.src[q];
+                if (src < 0) break;  // wave-uniform
                 const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, src);
                 const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), src) << 32) |
                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
                 const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
                 const u64 ce = tk_equal_of(c);
-                const u64 take_e = be >= need ? 0 : (need - be < ce ? need - be : ce);
-                const uint32_t total = tk_better_of(c) + (uint32_t)take_e;  // this tile's output keys
-                const u64 start = bb + (be < need ? be : need);            // and where they go
-                const u64 tb = t[q] * TK_TILE;
+                const u64 room = be >= need ? 0 : need - be;               // ties this tile may take
+                const uint32_t cap = (uint32_t)(room < 0xFFFFu ? room : 0xFFFFu);
+                const uint32_t total = tk_better_of(c) + (uint32_t)(room < ce ? room : ce);  // output keys
+                const u64 start = bb + (be < need ? be : need);             // and where they go
+                const u64 tb = (tg + (u64)src) * TK_TILE;
                 uint32_t mb = 0, me = 0;  // bit j: this lane's key j is better / equal
 #pragma unroll
                 for (int j = 0; j < TK_KPL; ++j) {
-                    const bool in = tb + tkw_col(lane, j) < n;
-                    const uint32_t u = key_of_i32(x[q][j]);
+                    const bool in = tb + TK_TILE <= n || tb + (u64)lane * TK_KPL + j < n;
+                    const uint32_t u = key_of_i32(cur.x[q][j]);
                     mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
                     me |= (uint32_t)(in && u == uv) << j;
                 }
-                // place the kept keys of key group g (the lane's keys g * G .. g * G + G - 1, in
-                // the tile's order after the lanes before it): b_before / e_before count the
-                // group's better / equal keys before this lane's
-                auto place = [&](int g0, int G, u64 b_before, u64 e_before) {
-                    for (int j = g0; j < g0 + G; ++j) {
-                        u64 pos = ~0ull;
-                        if ((mb >> j) & 1) {
-                            pos = b_before + (e_before < need ? e_before : need);
-                            ++b_before;
-                        } else if ((me >> j) & 1) {
-                            if (e_before < need) pos = b_before + e_before;
-                            ++e_before;
-                        }
-                        if (pos != ~0ull) {
-                            const uint32_t r = (uint32_t)(pos - start);
-                            s_val[w][r] = x[q][j];
-                            s_col[w][r] = (uint16_t)tkw_col(lane, j);
-                        }
-                    }
-                };
-                if constexpr (TKW_COAL) {
-                    u64 b_run = bb, e_run = be;  // the rows before this one
+                const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
+                const uint32_t p = wave_incl_scan32(mine) - mine;
+                if (mb | me) {
+                    uint32_t pb = p & 0xFFFFu, pe = p >> 16;
 #pragma unroll
-                    for (int r = 0; r < TK_KPL / 4; ++r) {
-                        const uint32_t mine = (uint32_t)__popc((mb >> (4 * r)) & 0xFu) |
-                                              ((uint32_t)__popc((me >> (4 * r)) & 0xFu) << 16);
-                        const uint32_t incl = wave_incl_scan32(mine), p = incl - mine;
-                        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
-                        if (((mb | me) >> (4 * r)) & 0xFu) place(4 * r, 4, b_run + (p & 0xFFFFu), e_run + (p >> 16));
-                        b_run += tot & 0xFFFFu;
-                        e_run += tot >> 16;
+                    for (int j = 0; j < TK_KPL; ++j) {
+                        const uint32_t isb = (mb >> j) & 1u, ise = (me >> j) & 1u;
+                        const uint32_t r = pb + min(pe, cap);
+                        if (isb | (ise & (uint32_t)(pe < cap))) {
+                            s_val[w][r] = cur.x[q][j];
+                            s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                        }
+                        pb += isb;
+                        pe += ise;
                     }
-                } else {
-                    const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
-                    const uint32_t p = wave_incl_scan32(mine) - mine;
-                    if (mb | me) place(0, TK_KPL, bb + (p & 0xFFFFu), be + (p >> 16));
                 }
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
