@@ -327,7 +327,15 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 #endif
 constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
 template <bool ALIGNED, bool STAGED = false>
-__global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
+#ifndef KTH_TKW_WAVES  // design exploration: minimum waves per SIMD the compiler must fit (0: its choice)
+#define KTH_TKW_WAVES 0
+#endif
+#if KTH_TKW_WAVES
+#define KTH_TKW_BOUNDS __launch_bounds__(TK_BLOCK, KTH_TKW_WAVES)
+#else
+#define KTH_TKW_BOUNDS __launch_bounds__(TK_BLOCK)
+#endif
+__global__ KTH_TKW_BOUNDS void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          const uint32_t *__restrict__ tcnt,
                                                          const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
