@@ -618,6 +618,10 @@ __device__ __forceinline__ void pick_slot(SelState &ss, const u64 *slot, bool sh
 // STORE = false: the chunk's keys only go into the histogram (the sample is
 // not kept: a later sample level re-reads the chunks from the input).
 // wg / nwg: this workgroup among the nwg that share the chunks.
+#ifndef KTH_HEAD_UNI
+#define KTH_HEAD_UNI 1
+#endif
+constexpr bool HEAD_UNI = KTH_HEAD_UNI != 0;  // the head's one-bin chunks as one atomic (below)
 template <int BLOCK, bool STORE = true>
 __device__ __forceinline__ bool gather_head_fast(const int32_t *__restrict__ keys, u64 stride, uint32_t *sample,
                                                  u64 s, uint32_t (*lh)[NBINS], const HistPlan &plan,
@@ -654,6 +658,20 @@ __device__ __forceinline__ bool gather_head_fast(const int32_t *__restrict__ key
                                                        0, 16 /* sc1: written through */);
             }
         }
+        // a chunk whose 1024 keys share one bin (sorted or few-valued input:
+        // consecutive keys, one digit) is one atomic, not 1024 serialised on
+        // one LDS address (sorted / all-equal 2^30: gather + first digit
+        // 16 us against 4.5 for uniform keys)
+        const uint32_t f = __builtin_amdgcn_readfirstlane((q[0].x >> sh) & mask);
+        bool same = true;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            same = same && ((q[r].x >> sh) & mask) == f && ((q[r].y >> sh) & mask) == f &&
+                   ((q[r].z >> sh) & mask) == f && ((q[r].w >> sh) & mask) == f;
+        if (HEAD_UNI && __ballot(!same) == 0) {  // wave-uniform
+            if (lane == 0) atomicAdd(&h[f], (uint32_t)SAMPLE_CHUNK);
+            continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             atomicAdd(&h[(q[r].x >> sh) & mask], 1u);
@@ -674,11 +692,38 @@ __device__ __forceinline__ void head_hist_chunks(const int32_t *__restrict__ key
     const int lane = threadIdx.x & (WAVE - 1);
     const u64 nchunks = s / SAMPLE_CHUNK;
     const u64 gw = ((u64)wg * BLOCK + threadIdx.x) / WAVE, nw = (u64)nwg * (BLOCK / WAVE);
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    // a key's bin for target t, or NONE (no histogram / prefix mismatch)
+    auto code = [&](uint32_t key, int t) {
+        const uint32_t v = key - plan.base;
+        return plan.h[t] && prefix_match(v, plan.W, plan.done[t], plan.prefix[t])
+                   ? (v >> plan.shift[t]) & plan.mask[t]
+                   : NONE;
+    };
     for (u64 c = gw; c < nchunks; c += nw) {  // wave-convergent
         const uint4 *src = reinterpret_cast<const uint4 *>(keys + c * stride);
         uint4 q[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) q[r] = src[r * WAVE + lane];
+        // the whole chunk in one bin per target (sorted / few-valued input):
+        // one atomic per target (as in gather_head_fast)
+        const uint32_t f0 = __builtin_amdgcn_readfirstlane(code(q[0].x ^ 0x80000000u, 0)),
+                       f1 = __builtin_amdgcn_readfirstlane(code(q[0].x ^ 0x80000000u, 1));
+        bool same = true;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t k4[4] = {q[r].x ^ 0x80000000u, q[r].y ^ 0x80000000u, q[r].z ^ 0x80000000u,
+                                    q[r].w ^ 0x80000000u};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) same = same && code(k4[j], 0) == f0 && code(k4[j], 1) == f1;
+        }
+        if (HEAD_UNI && __ballot(!same) == 0) {  // wave-uniform
+            if (lane == 0) {
+                if (f0 != NONE) atomicAdd(&lh[0][f0], (uint32_t)SAMPLE_CHUNK);
+                if (f1 != NONE) atomicAdd(&lh[1][f1], (uint32_t)SAMPLE_CHUNK);
+            }
+            continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             hist_add<BLOCK>(lh, plan, q[r].x ^ 0x80000000u, true);
