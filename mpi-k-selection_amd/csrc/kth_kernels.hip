@@ -1468,7 +1468,17 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
 #pragma unroll
                 for (int q = 0; q < BLK / WAVE; ++q) {
                     const uint32_t nq = (uint32_t)red[4][q];
-                    for (uint32_t i = threadIdx.x; i < nq; i += BLK) atomicAdd(&phist[(region[q][i] - base) >> sh], 1u);
+                    for (uint32_t i = threadIdx.x; i < nq; i += BLK) {
+                        // a wave-instruction's candidates in one bin (sorted input:
+                        // a workgroup's candidates are a run of values) add once
+                        const uint32_t b = (region[q][i] - base) >> sh, f = __builtin_amdgcn_readfirstlane(b);
+                        const u64 act = __ballot(true);
+                        if (HEAD_UNI && __ballot(b != f) == 0) {
+                            if ((uint32_t)lane == (uint32_t)__builtin_ctzll(act)) atomicAdd(&phist[f], (uint32_t)__popcll(act));
+                        } else {
+                            atomicAdd(&phist[b], 1u);
+                        }
+                    }
                 }
                 __syncthreads();
                 uint32_t *dst = a.pre_hist + (blockIdx.x % PRE_COPIES) * PRE_BINS;
