@@ -107,8 +107,6 @@ struct kth_ctx {
     uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
     int fin_set = 0;           // k_finish slot set of the next launch (the other one is cleared by it)
     bool pre_hist = true;      // k_main<0> histograms the candidates' first digit for k_finish (KTH_PRE_HIST=0: off)
-    int tkw_per_cu = 16;       // k_topk_write's grid: workgroups per CU at most (KTH_TKW_GRID)
-    int tkw_lds = 0;           // ... and extra dynamic LDS per workgroup, bytes (KTH_TKW_LDS: fewer resident)
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cu = 256;
@@ -714,8 +712,6 @@ int kth_ctx_create(int device, kth_ctx **out) {
             if (const char *g = getenv("KTH_POST_SPARSE_GRID")) c->post_sparse_grid = std::max(1, atoi(g));
             if (const char *g = getenv("KTH_COOP")) c->coop = atoi(g) != 0;
             if (const char *g = getenv("KTH_PRE_HIST")) c->pre_hist = atoi(g) != 0;
-            if (const char *g = getenv("KTH_TKW_GRID")) c->tkw_per_cu = std::max(1, atoi(g));
-            if (const char *g = getenv("KTH_TKW_LDS")) c->tkw_lds = std::max(0, std::min(atoi(g), 128 * 1024));
             c->fin_grid = c->num_cu;
             if (const char *g = getenv("KTH_FIN_GRID")) c->fin_grid = std::max(1, std::min(atoi(g), c->num_cu));
             if (const char *g = getenv("KTH_HEAD_SLACK")) c->head_slack64 = (uint32_t)std::max(0.0, atof(g) * 64.0);
@@ -1090,7 +1086,6 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
     // count and write passes: one wave per 64 tiles
     const int waves = kth::TK_BLOCK / kth::WAVE;
     const int g = (int)std::min<u64>((ntiles + waves * kth::WAVE - 1) / (waves * kth::WAVE), (u64)c->num_cu * 16);
-    const int gw = (int)std::min<u64>((u64)g, (u64)c->num_cu * c->tkw_per_cu);  // the write pass's grid
     if (tf >= 5) {  // the staged entries (rows < ncov), then the ragged rows from the input
         auto tk5c = (u64)k * 64 >= (u64)n ? kth::k_tk5_count<true> : kth::k_tk5_count<false>;  // dense windows: chunked
         tk5c<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
@@ -1150,14 +1145,14 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         tk5w<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
             c->tk_segv, c->tk_segp, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status,
             flip, c->tk_wcnt, tcnt, toff, bbase, meta, d_vals, d_idx);
-        kth::k_topk_write<true, true><<<gw, kth::TK_BLOCK, (size_t)c->tkw_lds, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+        kth::k_topk_write<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                           tcnt, toff, bbase, meta, d_vals, d_idx,
                                                                           tflags, ncov);
     } else if (aligned)
-        kth::k_topk_write<true><<<gw, kth::TK_BLOCK, (size_t)c->tkw_lds, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+        kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                     toff, bbase, meta, d_vals, d_idx);
     else
-        kth::k_topk_write<false><<<gw, kth::TK_BLOCK, (size_t)c->tkw_lds, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+        kth::k_topk_write<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
                                                                      toff, bbase, meta, d_vals, d_idx);
     return launch_check();
 }

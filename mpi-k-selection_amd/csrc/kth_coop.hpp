@@ -239,10 +239,12 @@ __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPla
 
 // The tail of k_finish: once a level's picked bin holds <= FIN_LDS_KEYS keys,
 // the remaining digits need no more grid barriers.  Every workgroup appends
-// its slice's keys of that bin to x.tail (one reservation on the tail word's
-// low half), then arrives on its high half; the workgroup that arrives last
-// holds every key in the tail, loads them into its LDS and resolves the
-// remaining digits alone, with block barriers only.  (A grid level costs ~10
+// its slice's keys of that bin to x.tail: one atomic on the tail word adds
+// its key count to the low half (its offset) and its arrival to the high half;
+// each writes its keys and then counts itself written (a non-returning add).
+// The workgroup that reserved last waits until the others are written, loads
+// every key of the tail into its LDS and resolves the remaining digits alone,
+// with block barriers only.  (A grid level costs ~10
 // us: flush round trip + barrier + pick; the tail ~3 round trips.)  One CU
 // scans ~0.6 keys a clock (a 64-lane VALU op takes 4 clocks), so every pass
 // over keys here is lean: one scan of the slice (staged in LDS), 16-byte LDS
@@ -250,16 +252,12 @@ __device__ __forceinline__ void finish_keys(uint32_t (*lh)[NBINS], const HistPla
 // workgroup that finished.  Keys go to x.tail as order keys (xr: the domain
 // is the raw int32 input).
 constexpr uint32_t TAIL_STAGE = 2 * NBINS;  // keys a workgroup stages in LDS (the histogram's space)
-#ifndef KTH_TAIL_ONE_RT
-#define KTH_TAIL_ONE_RT 1
-#endif
-// one atomic reserves and arrives (see finish_tail): select 0.6769 -> 0.6749 ms
-// (4 interleaved rounds, one box); the two-atomic form stays as
-// KTH_TAIL_ONE_RT=0.  (Loading k_finish's slice by LDS-DMA instead of
-// registers when PreHist gives the first digit measured equal, 0.6729 vs
-// 0.6723 ms: the slice lands ~3.5 us after the decide either way; reading and
-// picking PreHist takes ~4 us more, profiles/r5_select_stamps.txt.)
-constexpr bool TAIL_ONE_RT = KTH_TAIL_ONE_RT != 0;
+// One atomic reserves and arrives (see finish_tail): select 0.6769 -> 0.6749
+// ms against a reservation and then an arrival (4 interleaved rounds, one
+// box).  (Loading k_finish's slice by LDS-DMA instead of registers when
+// PreHist gives the first digit measured equal, 0.6729 vs 0.6723 ms: the
+// slice lands ~3.5 us after the decide either way; reading and picking
+// PreHist takes ~4 us more, profiles/r5_select_stamps.txt.)
 
 __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, uint4 *res, u64 nk, bool xr,
                             uint32_t (*lh)[NBINS], u64 *scratch) {
@@ -304,15 +302,11 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
     }
     __syncthreads();
     const uint32_t n_mine = s_n;
-    if (threadIdx.x == 0) {
-        if (TAIL_ONE_RT) {  // the reservation is the arrival: one round trip
-            const u64 old = __hip_atomic_fetch_add(ctl, (1ull << 32) | n_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_off = (uint32_t)old;
-            s_last = (uint32_t)(old >> 32) == gridDim.x - 1u;
-            s_total = (uint32_t)old + n_mine;
-        } else {
-            s_off = n_mine ? __hip_atomic_fetch_add(ctl, (u64)n_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
+    if (threadIdx.x == 0) {  // the reservation is the arrival: one round trip
+        const u64 old = __hip_atomic_fetch_add(ctl, (1ull << 32) | n_mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_off = (uint32_t)old;
+        s_last = (uint32_t)(old >> 32) == gridDim.x - 1u;
+        s_total = (uint32_t)old + n_mine;
     }
     __syncthreads();
     const uint32_t off = (uint32_t)s_off;
@@ -340,43 +334,31 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
     }
     wait_mem();
     __syncthreads();
-    if (TAIL_ONE_RT) {
-        // the others' keys are in once each has counted itself written (a
-        // non-returning add after its stores are performed); the last to
-        // reserve waits for that, bounded, and resets both words
-        uint32_t *written = x.bar + BAR_TAIL + 32;
-        if (!s_last) {
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(written, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            KTH_STAMP(a, 5);
-            return false;
-        }
-        if (threadIdx.x == 0) {
-            uint32_t spins = 0;
-            while (__hip_atomic_load(written, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x - 1u) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins >= BAR_SPIN_LIMIT) {
-                    ss.error = ERR_BARRIER;
-                    ss.mode = MODE_DONE;
-                    break;
-                }
-            }
-            __hip_atomic_store(written, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next select
-            __hip_atomic_store(ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
+    // the others' keys are in once each has counted itself written (a
+    // non-returning add after its stores are performed); the last to
+    // reserve waits for that, bounded, and resets both words
+    uint32_t *written = x.bar + BAR_TAIL + 32;
+    if (!s_last) {
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(written, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         KTH_STAMP(a, 5);
-        if (ss.error) return true;  // block-uniform (the state carries the timeout)
-    } else {
-        if (threadIdx.x == 0) {
-            const u64 old = __hip_atomic_fetch_add(ctl, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = (uint32_t)(old >> 32) == gridDim.x - 1u;
-            s_total = (uint32_t)old;
-            if (s_last) __hip_atomic_store(ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next select
-        }
-        __syncthreads();
-        KTH_STAMP(a, 5);
-        if (!s_last) return false;
+        return false;
     }
+    if (threadIdx.x == 0) {
+        uint32_t spins = 0;
+        while (__hip_atomic_load(written, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gridDim.x - 1u) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins >= BAR_SPIN_LIMIT) {
+                ss.error = ERR_BARRIER;
+                ss.mode = MODE_DONE;
+                break;
+            }
+        }
+        __hip_atomic_store(written, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next select
+        __hip_atomic_store(ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    KTH_STAMP(a, 5);
+    if (ss.error) return true;  // block-uniform (the state carries the timeout)
     const uint32_t total = s_total;
     if (total > (uint32_t)FIN_LDS_KEYS) {  // cannot happen: the bin's reduced count was checked
         if (threadIdx.x == 0) {

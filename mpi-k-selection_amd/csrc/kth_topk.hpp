@@ -172,17 +172,10 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_count(const uint32_t *__restr
 // (~6 candidates a row at 2^30) share a few cache lines of the counts.  (Runs
 // of 8 consecutive candidates per lane, one atomic per run of equal rows:
 // fewer atomics, but each instruction's spread over ~64 lines: 68 us.)
-// TKC_SEG: one atomic per run of equal rows among a wave-instruction's 64
+// Then one atomic per run of equal rows among a wave-instruction's 64
 // (k = 2^27 / 2^29: 34 / 42 us against 50 / 105 for one per candidate, and
 // 48 / 102 with one candidate a lane).
-#ifndef KTH_TKC_U
-#define KTH_TKC_U 8
-#endif
-constexpr int TKC_U = KTH_TKC_U;  // candidates a lane loads together
-#ifndef KTH_TKC_SEG
-#define KTH_TKC_SEG 1
-#endif
-constexpr bool TKC_SEG = KTH_TKC_SEG != 0;  // one atomic per run of equal rows in a wave (see there)
+constexpr int TKC_U = 8;  // candidates a lane loads together
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restrict__ cand,
                                                          const uint32_t *__restrict__ rows,
                                                          const u64 *__restrict__ cand_count, u64 cap,
@@ -207,7 +200,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restr
 #pragma unroll
         for (int q = 0; q < TKC_U; ++q) {
             const uint32_t c = tk_better(u[q], uv, flip) ? 1u : (u[q] == uv ? 0x10000u : 0u);
-            if (TKC_SEG) {
+            {
                 // one atomic per run of equal rows among the wave's 64: the
                 // run's last lane adds (prefix sum here) - (prefix sum at the
                 // run before); prefix sums never decrease (fields <= 64), so
@@ -224,9 +217,8 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restr
                 T = max(T, dpp32<0x143, 0xC>(T));
                 const uint32_t before = (uint32_t)__shfl_up((int)T, 1, WAVE);
                 const uint32_t add = S - (lane == 0 ? 0u : before);
+                // (~0u: past m, or outside k_main's rows: counted from the input)
                 if (last && r[q] != ~0u && add) atomicAdd(&tcnt[r[q]], add);
-            } else if (r[q] != ~0u && c) {  // (~0u: past m, or outside k_main's rows: counted from the input)
-                atomicAdd(&tcnt[r[q]], c);
             }
         }
     }
@@ -327,15 +319,7 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restri
 #endif
 constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
 template <bool ALIGNED, bool STAGED = false>
-#ifndef KTH_TKW_WAVES  // design exploration: minimum waves per SIMD the compiler must fit (0: its choice)
-#define KTH_TKW_WAVES 0
-#endif
-#if KTH_TKW_WAVES
-#define KTH_TKW_BOUNDS __launch_bounds__(TK_BLOCK, KTH_TKW_WAVES)
-#else
-#define KTH_TKW_BOUNDS __launch_bounds__(TK_BLOCK)
-#endif
-__global__ KTH_TKW_BOUNDS void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          const uint32_t *__restrict__ tcnt,
                                                          const u64 *__restrict__ toff, const u64 *__restrict__ bbase,
