@@ -113,6 +113,12 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     KTH_STAMP(a, 0);
     GridBar gb = grid_bar_init(x.bar, s_base);
     for (int i = threadIdx.x; i < 2 * NBINS / 4; i += DENSE_BLK) reinterpret_cast<uint4 *>(&lh[0][0])[i] = make_uint4(0, 0, 0, 0);
+    // the streaming pass's count slot and the candidate count: k_finish of the
+    // previous select read them last and nothing here reads them, so every
+    // workgroup clears its share first, under the gather (workgroup 0 alone
+    // clearing them at the end: the same select time, 4 interleaved rounds)
+    for (u64 i = (u64)blockIdx.x * DENSE_BLK + threadIdx.x; i < a.zero_words; i += (u64)gridDim.x * DENSE_BLK)
+        a.stats_zero[i] = 0;
     advance<DENSE_BLK>(ss, a, scratch);
     bool share;
     HistPlan plan = make_plan(ss, &share);
@@ -199,9 +205,6 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
         *a.st_out = o;
     }
     grid_bar_finish(gb, s_base);
-    // the streaming pass's count slot and the candidate count (k_finish read them last)
-    if (blockIdx.x == 0)
-        for (u64 i = threadIdx.x; i < a.zero_words; i += DENSE_BLK) a.stats_zero[i] = 0;
     KTH_STAMP(a, 7);
 }
 
