@@ -1134,12 +1134,12 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
             }
         }
     }
-    kth::k_topk_reduce<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, bsum);
-    // a bracket failure (counts that do not hold the k-th) lands in the select's
-    // state, where kth_ctx_last_stats reports it as .error
-    kth::k_topk_scan<<<1, kth::TK_SCAN_BLOCK, 0, c->stream>>>(bsum, (int)nblk, (u64)k, bbase, meta,
-                                                              c->st + c->last_state);
-    kth::k_topk_down<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(tcnt, ntiles, toff);
+    // tile offsets, block bases and need in one launch (a bracket failure --
+    // counts that do not hold the k-th -- lands in the select's state, where
+    // kth_ctx_last_stats reports it as .error)
+    kth::k_topk_bases<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(
+        tcnt, ntiles, toff, bsum, (u64)k, bbase, meta, c->st + c->last_state,
+        reinterpret_cast<uint32_t *>(c->islots + BAR_OFF) + kth::BAR_TAIL + 48);
     if (tf >= 5) {
         auto tk5w = (u64)k * 32 <= (u64)n ? kth::k_tk5_write<kth::TK5_STAGE_SMALL> : kth::k_tk5_write<kth::TK5_STAGE_LARGE>;
         tk5w<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(

@@ -9,9 +9,9 @@
 //   k_topk_count   per tile, #better-than-v | #equal << 16; reads only the
 //                  tiles the select's own streaming pass flagged as possibly
 //                  holding output (k_main<TF>), all tiles otherwise
-//   k_topk_reduce  per 4096 tiles: the block's two sums
-//   k_topk_scan    one workgroup: exclusive block bases, need = k - #better
-//   k_topk_down    per 4096 tiles: each tile's offsets inside its block
+//   k_topk_bases   per 4096 tiles: each tile's offsets inside its block and
+//                  the block's sums; the last workgroup: exclusive block
+//                  bases, need = k - #better
 //   k_topk_write   per tile that holds an output key: wave scan + scatter;
 //                  tiles without output never load their keys.
 // A kept key's slot is (#better before it) + min(#equal before it, need).
@@ -23,7 +23,6 @@ namespace kth {
 constexpr int TK_BLOCK = 256;
 constexpr int TK_TILE = 1024;                     // keys per wave tile
 constexpr int TK_KPL = TK_TILE / WAVE;            // 16 keys per lane
-constexpr int TK_SCAN_BLOCK = 1024;
 constexpr int TK_TILES_PER_BLOCK = TK_BLOCK * 16;  // reduce / down-sweep granularity (4096 tiles)
 // scratch (u64 words): tile counts (u32, ntiles), tile offsets (u64, ntiles),
 // block sums (2 per block), block bases (2 per block), meta [need, error]
@@ -224,80 +223,73 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_cands(const uint32_t *__restr
     }
 }
 
-// Pass 2: block b sums tiles [4096 b, 4096 b + 4096) -> bsum[2b] (better), bsum[2b+1] (equal).
-__global__ __launch_bounds__(TK_BLOCK) void k_topk_reduce(const uint32_t *__restrict__ tcnt, u64 ntiles,
-                                                          u64 *__restrict__ bsum) {
-    const u64 t0 = (u64)blockIdx.x * TK_TILES_PER_BLOCK + threadIdx.x * 16;
-    u64 s = 0;
-    for (int j = 0; j < 16; ++j)
-        if (t0 + j < ntiles) {
-            const uint32_t c = tcnt[t0 + j];
-            s += tk_better_of(c) | ((u64)tk_equal_of(c) << 32);
-        }
-    __shared__ u64 wsum[TK_BLOCK / WAVE];
-    u64 tot;
-    block_exclusive_scan<TK_BLOCK>(s, wsum, &tot);  // per block < 2^32 keys: the halves cannot carry
-    if (threadIdx.x == 0) {
-        bsum[2 * blockIdx.x] = tot & 0xFFFFFFFFull;
-        bsum[2 * blockIdx.x + 1] = tot >> 32;
-    }
-}
-
-// Pass 3: one workgroup: bbase[2b], bbase[2b+1] = exclusive prefixes of the
-// better / equal block sums; meta[0] = need = k - #better; meta[1] = error
-// when the counts do not bracket k (cannot happen for a correct v).  The error
-// is also raised in the select's state (SelState.error = TK_ERR_BRACKET), which
-// kth_ctx_last_stats reports; k_topk_write then writes nothing.
+// A bracket failure (counts that do not hold the k-th; cannot happen for a
+// correct v) is raised in the select's state (SelState.error =
+// TK_ERR_BRACKET), which kth_ctx_last_stats reports; k_topk_write then
+// writes nothing (meta[1]).
 constexpr uint32_t TK_ERR_BRACKET = 32;
-__global__ __launch_bounds__(TK_SCAN_BLOCK) void k_topk_scan(const u64 *__restrict__ cnt, int G, u64 k,
-                                                             u64 *__restrict__ base, u64 *__restrict__ meta,
-                                                             SelState *__restrict__ st) {
-    const int per = (G + TK_SCAN_BLOCK - 1) / TK_SCAN_BLOCK;
-    const int g0 = threadIdx.x * per;
-    u64 sb = 0, se = 0;
-    for (int j = 0; j < per; ++j)
-        if (g0 + j < G) {
-            sb += cnt[2 * (g0 + j)];
-            se += cnt[2 * (g0 + j) + 1];
-        }
-    __shared__ u64 wsum[TK_SCAN_BLOCK / WAVE];
-    u64 tb, te;
-    u64 pb = block_exclusive_scan<TK_SCAN_BLOCK>(sb, wsum, &tb);
-    u64 pe = block_exclusive_scan<TK_SCAN_BLOCK>(se, wsum, &te);
-    for (int j = 0; j < per; ++j)
-        if (g0 + j < G) {
-            base[2 * (g0 + j)] = pb;
-            base[2 * (g0 + j) + 1] = pe;
-            pb += cnt[2 * (g0 + j)];
-            pe += cnt[2 * (g0 + j) + 1];
-        }
-    if (threadIdx.x == 0) {
-        const bool ok = tb < k && k <= tb + te;
-        meta[0] = ok ? k - tb : 0;
-        meta[1] = ok ? 0 : 1;
-        if (!ok && st) st->error = TK_ERR_BRACKET;
-    }
-}
 
-// Pass 4: toff[t] = (#better | #equal << 32) in the tiles of t's block before t.
-__global__ __launch_bounds__(TK_BLOCK) void k_topk_down(const uint32_t *__restrict__ tcnt, u64 ntiles,
-                                                        u64 *__restrict__ toff) {
+// Pass 2 (k_topk_bases, one workgroup per 4096 tiles): each
+// workgroup writes its tiles' in-block offsets (toff) and its
+// block's two sums (bsum, write-through), then arrives on a counter; the
+// last to arrive scans the block sums into the block bases and meta (as
+// a one-workgroup scan) and resets the counter.  (Round 4 had three
+// launches here: block sums, the scan of them, the in-block offsets.)
+__global__ __launch_bounds__(TK_BLOCK) void k_topk_bases(const uint32_t *__restrict__ tcnt, u64 ntiles,
+                                                         u64 *__restrict__ toff, u64 *__restrict__ bsum,
+                                                         u64 k, u64 *__restrict__ base, u64 *__restrict__ meta,
+                                                         SelState *__restrict__ st, uint32_t *__restrict__ arrive) {
+    __shared__ u64 wsum[TK_BLOCK / WAVE];
+    __shared__ uint32_t s_last;
     const u64 t0 = (u64)blockIdx.x * TK_TILES_PER_BLOCK + threadIdx.x * 16;
-    u64 v[16], s = 0;
+    u64 v[16], sm = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t c = t0 + j < ntiles ? tcnt[t0 + j] : 0u;
         v[j] = tk_better_of(c) | ((u64)tk_equal_of(c) << 32);
-        s += v[j];
+        sm += v[j];
     }
-    __shared__ u64 wsum[TK_BLOCK / WAVE];
-    u64 p = block_exclusive_scan<TK_BLOCK>(s, wsum, nullptr);
+    u64 tot;
+    u64 p = block_exclusive_scan<TK_BLOCK>(sm, wsum, &tot);  // per block < 2^32 keys: the halves cannot carry
 #pragma unroll
     for (int j = 0; j < 16; ++j)
         if (t0 + j < ntiles) {
             toff[t0 + j] = p;
             p += v[j];
         }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&bsum[2 * blockIdx.x], tot & 0xFFFFFFFFull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bsum[2 * blockIdx.x + 1], tot >> 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wait_mem();
+        s_last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!s_last) return;  // block-uniform
+    // the last workgroup: exclusive bases of the block sums, need and the bracket check
+    const int G = (int)gridDim.x, per = (G + TK_BLOCK - 1) / TK_BLOCK, g0 = threadIdx.x * per;
+    u64 sb = 0, se = 0;
+    for (int j = 0; j < per; ++j)
+        if (g0 + j < G) {
+            sb += __hip_atomic_load(&bsum[2 * (g0 + j)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            se += __hip_atomic_load(&bsum[2 * (g0 + j) + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    u64 tb, te;
+    u64 pb = block_exclusive_scan<TK_BLOCK>(sb, wsum, &tb);
+    u64 pe = block_exclusive_scan<TK_BLOCK>(se, wsum, &te);
+    for (int j = 0; j < per; ++j)
+        if (g0 + j < G) {
+            base[2 * (g0 + j)] = pb;
+            base[2 * (g0 + j) + 1] = pe;
+            pb += __hip_atomic_load(&bsum[2 * (g0 + j)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pe += __hip_atomic_load(&bsum[2 * (g0 + j) + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    if (threadIdx.x == 0) {
+        const bool ok = tb < k && k <= tb + te;
+        meta[0] = ok ? k - tb : 0;
+        meta[1] = ok ? 0 : 1;
+        if (!ok && st) st->error = TK_ERR_BRACKET;
+        *arrive = 0u;  // for the next call (every workgroup has arrived)
+    }
 }
 
 // Pass 5: ordered compaction.  Each wave looks at 64 tiles at once (one per
