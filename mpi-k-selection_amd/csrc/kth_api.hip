@@ -105,6 +105,7 @@ struct kth_ctx {
     bool coop_resident = true; // the cooperative grids fit the device at once (occupancy check at ctx creation)
     int fin_grid = 256;        // k_finish workgroups (one per CU; KTH_FIN_GRID)
     uint32_t head_slack64 = (uint32_t)(HEAD_SLACK * 64);
+    uint32_t head_abs_div = 1024;  // plain select: early-window floor s / head_abs_div sample keys (KTH_HEAD_ABS; 0 = off)
     int fin_set = 0;           // k_finish slot set of the next launch (the other one is cleared by it)
     bool pre_hist = true;      // k_main<0> histograms the candidates' first digit for k_finish (KTH_PRE_HIST=0: off)
     hipStream_t stream = nullptr;
@@ -470,8 +471,17 @@ int run_window(kth_ctx *c, const int32_t *keys, int64_t n, int64_t k, int32_t *d
         a.init_s = (u64)s;
         a.r_lo = r_lo;
         a.r_hi = r_hi;
-        kth::k_head<<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, coop_args(c, HSLOT_OFF, nullptr, nullptr),
-                                                                          keys, (u64)n, stride, c->sample, (u64)s);
+        // the plain select takes a first-level window of up to s / head_abs_div
+        // sample keys (~n / 1024 candidates) whatever the slack: at k near 1 or
+        // n it spares the second sample level (the top-k variants keep the
+        // narrow window: their count pass loads the rows below its far edge).
+        // Sorted input at k = 1 / n: 0.672-0.675 -> 0.654-0.658 ms; uniform
+        // keys unchanged (their edge bin holds ~1024 sample keys: s / 256 took
+        // them, ~1 M candidates, and cost ~10 us more than the level saves)
+        kth::CoopArgs hx = coop_args(c, HSLOT_OFF, nullptr, nullptr);
+        if (tflag == 0 && c->head_abs_div) hx.abs_min = (u64)s / c->head_abs_div;
+        kth::k_head<<<gather_grid(nchunks), kth::DENSE_BLK, 0, c->stream>>>(a, hx, keys, (u64)n, stride, c->sample,
+                                                                          (u64)s);
         // the streaming pass: counts into islot(1) (zero between selects);
         // the plain pass also histograms the candidates' first digit for k_finish
         a = step(c, kth::ADV_CARRY, 0, 1, nullptr, islot(c, 1), nullptr);
@@ -715,6 +725,7 @@ int kth_ctx_create(int device, kth_ctx **out) {
             c->fin_grid = c->num_cu;
             if (const char *g = getenv("KTH_FIN_GRID")) c->fin_grid = std::max(1, std::min(atoi(g), c->num_cu));
             if (const char *g = getenv("KTH_HEAD_SLACK")) c->head_slack64 = (uint32_t)std::max(0.0, atof(g) * 64.0);
+            if (const char *g = getenv("KTH_HEAD_ABS")) c->head_abs_div = (uint32_t)std::max(0, atoi(g));
             // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
             // so its count pass must report the bracket failure
             c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;

@@ -29,6 +29,7 @@ struct CoopArgs {
     int32_t *d_out, *d_status;
     u64 dense_per_wg, sparse_per_wg;  // keys per active workgroup: first digit of a domain / later digits
     uint32_t slack64;  // k_head early window (EarlyWindow); 0 = exact sample ranks
+    u64 abs_min;       // ... and its absolute floor in sample keys (EarlyWindow::abs_min)
     u64 *zero2;        // k_finish: a second region to clear (the sample phase's slots)
     u64 zero2_words;
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(DENSE_BLK) void k_head(StepArgs a, CoopArgs x, cons
     wait_mem();
     KTH_STAMP(a, 6);
 #endif
-    const EarlyWindow ew{a.r_lo, a.r_hi, x.slack64};
+    const EarlyWindow ew{a.r_lo, a.r_hi, x.slack64, x.abs_min};
     bool ok = true;
     for (int L = 0;; ++L) {
         grid_sync(gb, s_base, ok);

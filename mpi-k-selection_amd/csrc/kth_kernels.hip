@@ -188,6 +188,7 @@ __device__ __forceinline__ void decide(SelState &s, const u64 *c) {
 struct EarlyWindow {
     u64 r_lo, r_hi;   // the sample ranks of the targets (0 / s+1: no bound)
     uint32_t slack64; // 0: off
+    u64 abs_min;      // a span of up to this many sample keys is taken whatever the slack (0: none)
 };
 
 __device__ __forceinline__ void early_window(SelState &s, const EarlyWindow &e, u64 cnt1) {
@@ -197,7 +198,7 @@ __device__ __forceinline__ void early_window(SelState &s, const EarlyWindow &e, 
     const u64 below0 = a0 ? e.r_lo - s.t[0].k : 0;           // sample keys under r_lo's bin
     const u64 upto1 = a1 ? e.r_hi - s.t[1].k + cnt1 : s.s;    // sample keys up to r_hi's bin's top
     const u64 want = (a1 ? e.r_hi : s.s) - (a0 ? e.r_lo : 1) + 1;
-    if (upto1 < below0 || (upto1 - below0) * 64 > want * (u64)e.slack64) return;
+    if (upto1 < below0 || ((upto1 - below0) * 64 > want * (u64)e.slack64 && upto1 - below0 > e.abs_min)) return;
     const uint32_t w0 = s.W - s.t[0].done, w1 = s.W - s.t[1].done;
     s.lo = a0 ? s.base + (w0 >= 32 ? 0u : s.t[0].prefix << w0) : 0u;
     s.hi = a1 ? s.base + (w1 >= 32 ? 0xFFFFFFFFu : (s.t[1].prefix << w1) | ((1u << w1) - 1u)) : 0xFFFFFFFFu;
