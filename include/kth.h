@@ -205,6 +205,14 @@ int kth_dist_window(kth_ctx *ctx, const uint32_t *d_sample, int64_t s_total);
 int kth_dist_scan(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local);
 int kth_dist_level(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, int level);
 int kth_dist_result(kth_ctx *ctx, int32_t *d_out);
+/* Optional, right after level 0's slot is all-reduced and before
+ * kth_dist_level(ctx, .., 1): enqueue the result as if level 0 were the last
+ * (it is when the window is at most 2^24 values wide or decided by its counts),
+ * so the device need not wait for the host's look at level 0's status.  If
+ * more levels follow, it writes nothing and the protocol goes on; the closing
+ * kth_dist_result with the same d_out is then the only launch that writes (and
+ * costs nothing when the early one finished the select). */
+int kth_dist_result_early(kth_ctx *ctx, int32_t *d_out);
 /* Sample size for n keys (the single-GPU rule: min(2^20, n/64), a multiple
  * of 64).  Sharded callers take about kth_dist_sample_size(n_total) / P keys
  * per rank (a multiple of 64, at least 64), so that the all-gathered sample

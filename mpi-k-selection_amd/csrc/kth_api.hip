@@ -156,6 +156,7 @@ struct kth_ctx {
     u64 dscan_per_wg = DSCAN_PER_WG;  // k_dscan_hist keys per workgroup (KTH_DSCAN_PER_WG)
     int dist_levels = -1;      // level calls that return a slot (from level 0's DistStatus; -1: unknown yet)
     int dist_result_slot = -1; // the slot the last level accumulated into (kth_dist_result reads it)
+    int32_t *dist_early_out = nullptr;  // kth_dist_result_early's answer buffer this select (null: none)
     uint32_t *h_dist = nullptr;  // DistStatus, host-visible (pinned, mapped), written by level 0's k_dlevel
     uint32_t *d_dist = nullptr;  // ... its device address
     hipEvent_t ev_dist = nullptr;  // recorded after level 0
@@ -1214,6 +1215,7 @@ int kth_dist_begin(kth_ctx *c, uint64_t *d_slots, int64_t n_total, int64_t k) {
     c->dist_level_next = -1;  // kth_dist_scan first
     c->dist_levels = -1;
     c->dist_result_slot = -1;
+    c->dist_early_out = nullptr;
     c->dist_zero = true;  // kth_dist_sample clears the slots inside its kernel
     // the ctx's own slots are left zeroed by every completed k_result; a
     // sequence cut short (dirty, or a dist selection never finished) re-zeroes,
@@ -1410,22 +1412,41 @@ int kth_internal_dist_window_share(kth_ctx *src, kth_ctx *const *dst, int P) {
     return KTH_OK;
 }
 
-int kth_dist_result(kth_ctx *c, int32_t *d_out) {
-    if (!c || !d_out || !c->uslots || c->dist_result_slot < 0) return KTH_EINVAL;
-    KTH_TRY(set_device(c));
-    const int L = c->dist_levels;  // levels enqueued: the last wrote state (L - 1) % 2
+// k_dresult after L levels: state (L + 1) % 2 and slot L % 3 in, the other state out
+static int launch_dresult(kth_ctx *c, int L, int32_t *d_out, uint32_t early) {
     const int st_in = (L + 1) % 2;
-    StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)c->dist_result_slot * KTH_STATS_WORDS,
+    StepArgs a = step(c, kth::ADV_PICK, st_in, 1 - st_in, c->uslots + (size_t)(L % 3) * KTH_STATS_WORDS,
                       nullptr, nullptr);
     // (the islots and, right after them, k_head's slots of a cooperative window)
     static_assert(ISLOT_WORDS % 2 == 0, "k_dresult zeroes 16-byte words from the islots on");
     kth::k_dresult<kth::BLK><<<16, kth::BLK, 0, c->stream>>>(a, d_out, c->d_status, c->islots,
-                                                            ISLOT_WORDS + HSLOT_WORDS);
+                                                            ISLOT_WORDS + HSLOT_WORDS, early);
     c->last_state = 1 - st_in;
+    return launch_check();
+}
+
+int kth_dist_result_early(kth_ctx *c, int32_t *d_out) {
+    // right after level 0's slot was all-reduced, before kth_dist_level(1):
+    // the result as if level 0 were the last (it is whenever the window is at
+    // most 2^24 values wide or decided by its counts)
+    if (!c || !d_out || !c->uslots || c->dist_level_next != 1 || c->dist_levels >= 0) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    KTH_TRY(launch_dresult(c, 1, d_out, 1u));
+    c->dist_early_out = d_out;
+    return KTH_OK;
+}
+
+int kth_dist_result(kth_ctx *c, int32_t *d_out) {
+    if (!c || !d_out || !c->uslots || c->dist_result_slot < 0) return KTH_EINVAL;
+    KTH_TRY(set_device(c));
+    const int L = c->dist_levels;  // levels enqueued: the last wrote state (L - 1) % 2
+    if (!(L == 1 && c->dist_early_out == d_out))  // else the early result did it
+        KTH_TRY(launch_dresult(c, L, d_out, 0u));
+    c->dist_early_out = nullptr;
     c->dist_level_next = -1;
     c->dist_result_slot = -1;
     c->dist_open = false;
-    return launch_check();
+    return KTH_OK;
 }
 
 }  // extern "C"

@@ -1763,14 +1763,21 @@ __global__ __launch_bounds__(BLOCK) void k_dlevel(StepArgs a) {
 // writes the answer (only a verified one reaches d_out); every workgroup
 // zeroes its share of the ctx-internal slots (16-byte stores).
 template <int BLOCK>
+// early (kth_dist_result_early: enqueued before the host knows how many levels
+// the protocol takes): every workgroup picks, and unless the pick finishes the
+// selection nothing is written or cleared -- the protocol then goes on and
+// its final k_dresult does the work.
 __global__ __launch_bounds__(BLOCK) void k_dresult(StepArgs a, int32_t *d_out, int32_t *d_status, u64 *izero,
-                                                   u64 izero_words) {
+                                                   u64 izero_words, uint32_t early) {
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (BLOCK / WAVE) + 8];
     __shared__ u64 cnts[NCOUNTS];
-    if (blockIdx.x == 0) {
+    if (blockIdx.x == 0 || early) {  // grid-uniform
         dist_state<BLOCK>(ss, a, cnts);
         dist_pick<BLOCK>(ss, a, scratch);
+        if (early && (ss.mode != MODE_DONE || ss.error)) return;  // block-uniform (the same pick in every block)
+    }
+    if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
             SelState o = ss;
             if (o.mode != MODE_DONE && !o.error) o.error = 16 + o.mode;

@@ -96,6 +96,11 @@ class HipBackend:
     def result(self, out):
         check(_lib.kth_dist_result(self.ctx, out.data_ptr()), "kth_dist_result")
 
+    def result_early(self, out):
+        """The result enqueued before level 1 looks at level 0's status (a
+        no-op on the device unless level 0 was the last); result() closes."""
+        check(_lib.kth_dist_result_early(self.ctx, out.data_ptr()), "kth_dist_result_early")
+
     def alloc_out(self):
         return torch.empty(1, dtype=torch.int32, device=self.device)
 
@@ -148,6 +153,10 @@ class DistSelector:
         i = b.scan(shard, n_local)  # counts + the candidates' first digit
         yield ("all_reduce", self.slots[i])
         for level in range(KTH_DIST_MAX_LEVELS + 1):  # usually one level: two all-reduces in all
+            if level == 1 and hasattr(b, "result_early") and os.environ.get("KTH_DIST_EARLY", "1") != "0":
+                # before level 1 waits for level 0's status on the host, so the
+                # device runs the (usual) last step right after the all-reduce
+                b.result_early(out)
             i = b.level(shard, n_local, level)
             if i == KTH_DIST_DONE:
                 break

@@ -34,7 +34,7 @@ def test_headers_declare_expected_api():
     k = declared_functions("kth.h")
     v = declared_functions("vector.h")
     for name in ("kth_select_i32", "kth_select_i32_async", "kth_ctx_create", "kth_select_rows_f32",
-                 "kth_dist_scan", "kth_dist_level", "kth_dist_result"):
+                 "kth_dist_scan", "kth_dist_level", "kth_dist_result", "kth_dist_result_early"):
         assert name in k
     # the reference's 18 prototypes (vector.h:13-33) + the drop-in select
     ref18 = ["VecNew", "VecAdd", "VecDelete", "VecErase", "MinFind", "MaxFind", "AverageFind", "VecGetCapacity",
