@@ -564,6 +564,7 @@ def main():
     keys = torch.empty(n_local * P, dtype=torch.int32, device=dev)
     sel.fill(keys, n_local * P, family, args.seed, offset=rank * n_local, n_total=n_total)
     out = torch.zeros(args.warmup + args.steps, dtype=torch.int32, device=dev)
+    outv = [out[i:i + 1] for i in range(args.warmup + args.steps)]  # (views made before any timing)
     comm_world = None
     local_answers = [0] * (args.warmup + args.steps)
 
@@ -583,7 +584,7 @@ def main():
         sel.reserve(n_local)
 
         def step(i):
-            sel.select_async(keys, n_local, k, out[i:i + 1])
+            sel.select_async(keys, n_local, k, outv[i])
     else:
         ds = DistSelector(HipBackend(local_rank, sel))
         comm_world = getattr(ds.comm, "world", None)
@@ -591,7 +592,7 @@ def main():
             raise SystemExit(f"bench: RCCL communicator spans {comm_world} ranks, WORLD_SIZE is {world}")
 
         def step(i):
-            ds.select(keys, n_local, n_total, k, out=out[i:i + 1])
+            ds.select(keys, n_local, n_total, k, out=outv[i])
 
     for i in range(args.warmup):
         step(i)

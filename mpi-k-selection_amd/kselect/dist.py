@@ -128,12 +128,17 @@ class DistSelector:
         self._sample = None
         self._gathered = None
         self._checked = None  # last (n_local, n_total, k) every rank agreed on
+        self._s_local_for, self._s_local, self._sample_n = None, 0, -1
 
     def s_local(self, n_total):
         """Sample keys per rank: the window needs ~sample_size(n_total) keys in
         all (what one GPU would take), not that many per rank, so the
-        all-gather stays ~4 MiB."""
-        return max(64, (self.b.sample_size(n_total) // self.world) & ~63)
+        all-gather stays ~4 MiB.  (Cached per n_total: the host's path between
+        two selects is what the device waits on when a select is short.)"""
+        if self._s_local_for != n_total:
+            self._s_local = max(64, (self.b.sample_size(n_total) // self.world) & ~63)
+            self._s_local_for = n_total
+        return self._s_local
 
     def steps(self, shard, n_local, n_total, k, out):
         """The per-rank protocol as a generator: the device steps run in the
@@ -143,9 +148,10 @@ class DistSelector:
         lockstep() performs them for P selectors in one process)."""
         b = self.b
         s_local = self.s_local(n_total)
-        if self._sample is None or self._sample.numel() != s_local:
+        if self._sample is None or self._sample_n != s_local:
             self._sample = b.alloc_sample(s_local)
             self._gathered = b.alloc_sample(s_local * self.world)
+            self._sample_n = s_local
         b.begin(self.slots, n_total, k)
         b.sample(shard, n_local, self._sample, s_local)
         yield ("all_gather", self._gathered, self._sample)
