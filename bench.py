@@ -64,19 +64,40 @@ def cpu_model():
 
 
 RDV_ENV = "KTH_RDV_FILE"  # launch_ranks' file rendezvous (no TCP port to probe and race for)
+# TEST MODE, not a scaling point: every rank on GPU 0, the collectives staged
+# through host memory over gloo (RCCL refuses two ranks on one device).  It runs
+# everything the multi-GPU launch depends on -- launcher, rendezvous, one ctx
+# per process, the sharded protocol with its early result and DistStatus read --
+# except RCCL's transport, on the one-GPU pool.
+SHARE_ENV = "KTH_SHARE_GPU"
+
+
+def shared_gpu():
+    return os.environ.get(SHARE_ENV, "0") not in ("", "0")
 
 
 def init_group(dev, backend="nccl"):
     """The ranks' process group: under torchrun (the driver's launch) env://
-    with the launcher's store; under launch_ranks a FileStore at $KTH_RDV_FILE."""
+    with the launcher's store; under launch_ranks a FileStore at $KTH_RDV_FILE.
+    Ranks sharing one GPU (KTH_SHARE_GPU=1) form a gloo group."""
     import torch.distributed as dist
 
+    if shared_gpu():
+        backend, dev = "gloo", None
     path = os.environ.get(RDV_ENV)
     if path:
         dist.init_process_group(backend, device_id=dev, init_method="file://" + path,
                                 rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
     else:
         dist.init_process_group(backend, device_id=dev)
+
+
+def coll_device(dev):
+    """Where the bench's own small collectives (timing max, certificate counts)
+    take tensors: host memory when the ranks share a GPU (gloo group)."""
+    import torch
+
+    return torch.device("cpu") if shared_gpu() else dev
 
 
 def launch_ranks(n, argv):
@@ -118,9 +139,12 @@ def launch_ranks(n, argv):
 
 
 def need_gpu(local_rank):
-    """Fail loudly (there is no CPU fallback) unless GPU `local_rank` is visible."""
+    """Fail loudly (there is no CPU fallback) unless GPU `local_rank` is visible
+    (GPU 0 for every rank when they share one, KTH_SHARE_GPU=1)."""
     import torch
 
+    if shared_gpu():
+        local_rank = 0
     ndev = torch.cuda.device_count() if torch.cuda.is_available() else 0
     if local_rank >= ndev:
         raise SystemExit(f"bench: rank needs GPU {local_rank} but {ndev} GPU(s) are visible (no CPU fallback)")
@@ -290,7 +314,7 @@ def rows_main(args):
     torch.cuda.set_stream(stream)
     if world > 1:
         init_group(dev)
-    sel = kselect.Selector(local_rank, stream=stream)
+    sel = kselect.Selector(dev.index, stream=stream)
     R, C = args.rows, args.cols
     k = args.k or C // 2
     f32 = args.rows_dtype == "f32"
@@ -332,7 +356,7 @@ def rows_main(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = sum(evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(args.steps)) / args.steps
@@ -415,7 +439,7 @@ def topk_main(args):
     torch.cuda.set_stream(stream)
     if world > 1:
         init_group(dev)
-    sel = kselect.Selector(local_rank, stream=stream)
+    sel = kselect.Selector(dev.index, stream=stream)
     n = 1 << args.log2n
     k = args.k or 1024
     keys = torch.empty(n, dtype=torch.int32, device=dev)
@@ -438,7 +462,7 @@ def topk_main(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     call_ms = sum(evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(args.steps)) / args.steps
@@ -552,7 +576,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    sel = kselect.Selector(local_rank)
+    sel = kselect.Selector(dev.index)
     sel.set_stream(torch.cuda.current_stream(dev))
     P = args.local_shards
     if P > 1 and sharded:
@@ -575,7 +599,7 @@ def main():
         # slot sum).  kth_sharded_select_i32 is synchronous: each step ends
         # with the answer on the host.
         views = [keys[i * n_local:(i + 1) * n_local] for i in range(P)]
-        sh = kselect.ShardedSelector([local_rank] * P)
+        sh = kselect.ShardedSelector([dev.index] * P)
         sizes = [n_local] * P
 
         def step(i):
@@ -586,7 +610,7 @@ def main():
         def step(i):
             sel.select_async(keys, n_local, k, outv[i])
     else:
-        ds = DistSelector(HipBackend(local_rank, sel))
+        ds = DistSelector(HipBackend(dev.index, sel))
         comm_world = getattr(ds.comm, "world", None)
         if comm_world != world:
             raise SystemExit(f"bench: RCCL communicator spans {comm_world} ranks, WORLD_SIZE is {world}")
@@ -620,7 +644,7 @@ def main():
     n_sel, main_ms, total_ms = sel.take_timing()
     sel.enable_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, elapsed_ev], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, elapsed_ev = (float(x) for x in t.tolist())
 
@@ -631,6 +655,7 @@ def main():
     for c in torch.split(keys, 1 << 30):  # (bounded temporaries at 2^33)
         cnt += torch.stack([(c < v).sum(), (c <= v).sum()]).to(torch.int64)
     if world > 1:
+        cnt = cnt.to(coll_device(dev))
         dist.all_reduce(cnt)
     lt, le = (int(x) for x in cnt.tolist())
     verified = (lt < k <= le) and all(a == v for a in answers)
@@ -649,11 +674,12 @@ def main():
     if P > 1:
         traffic, traffic_note = None, "PMC traffic is measured per k_main launch (one shard), not per sharded select"
 
+    shared = shared_gpu() and world > 1
     res = {
         "metric": "Gkeys/s exact k-th select, 2^30 int32 (1 GPU) / 2^33 (8 GPU); % HBM roofline",
         "value": value,
         "unit": "Gkeys/s",
-        "n_gpus": world,
+        "n_gpus": 1 if shared else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -670,8 +696,10 @@ def main():
             "k": k,
             "keys_per_gpu": n_local,
             "family": args.family,
-            "parallelism": f"shards{world}" if sharded else (f"local_shards{P}" if P > 1 else "single"),
-            "rccl_world": comm_world if sharded else None,
+            "parallelism": "shared-gpu-host-comm" if shared else (
+                f"shards{world}" if sharded else (f"local_shards{P}" if P > 1 else "single")),
+            "ranks": world,
+            "rccl_world": None if shared else (comm_world if sharded else None),
         },
         "roofline": {
             "bound": "hbm",
@@ -690,6 +718,10 @@ def main():
         "whole_select_ms_events": total_ms / max(1, n_sel) if not sharded else None,
         "ms_per_step_events": elapsed_ev * 1e3 / args.steps,
     }
+    if shared:
+        res["scaling_point"] = False
+        res["note"] = (f"TEST MODE (KTH_SHARE_GPU=1): {world} rank processes share GPU 0 and stage the collectives "
+                       "through host memory over gloo; not a scaling point (the host waits at every collective)")
     if stats:
         res["path"] = {1: "lds", 2: "radix", 3: "window", 4: "window_fallback"}.get(stats["path"], "?")
         res["candidates"] = stats["candidates"]

@@ -107,6 +107,23 @@ int kth_ctx_last_stats(kth_ctx *ctx, kth_stats *st);
  * redo the timed-out select; the asynchronous ones report it in the stats). */
 int kth_ctx_coop(const kth_ctx *ctx);
 
+/* --- test hooks (TEST ONLY: never set by the product path) ------------------
+ * Fault injectors for the parity tests' error paths.  They are off in every
+ * new ctx and are not read from the environment; only this call turns them on.
+ *   KTH_HOOK_FAULT_TOPK_RANK  value != 0: kth_topk_i32 selects a neighbouring
+ *                             rank, so its count pass must report the bracket
+ *                             failure (outputs unwritten, stats .error set)
+ *   KTH_HOOK_FAULT_BARRIER    1: every grid barrier of the cooperative kernels
+ *                             reports a timeout; 2: only the next cooperative
+ *                             launch does; 0: off
+ *   KTH_HOOK_TOPK_SEG_CAP     entries per staged top-k segment (0 = sized from n;
+ *                             small values force the segment-overflow fallback)
+ * Returns KTH_EINVAL for an unknown hook or a bad value. */
+#define KTH_HOOK_FAULT_TOPK_RANK 1
+#define KTH_HOOK_FAULT_BARRIER 2
+#define KTH_HOOK_TOPK_SEG_CAP 3
+int kth_ctx_test_hook(kth_ctx *ctx, int hook, int64_t value);
+
 /* --- timing (bench) ----------------------------------------------------------
  * When enabled, every select records HIP events on the ctx stream around the
  * streaming pass (the dominant kernel) and around the whole select. */
@@ -198,6 +215,9 @@ int kth_fill_synthetic(kth_ctx *ctx, int32_t *d_out, int64_t n, int64_t offset, 
 #define KTH_STATS_WORDS (8 + 2 * 2048)
 #define KTH_DIST_DONE 3
 #define KTH_DIST_MAX_LEVELS 3
+/* Deprecated (round-4 API): callers loop kth_dist_level until KTH_DIST_DONE;
+ * kept so that code written against the old name still builds. */
+#define KTH_DIST_LEVELS KTH_DIST_MAX_LEVELS
 int kth_dist_begin(kth_ctx *ctx, uint64_t *d_slots, int64_t n_total, int64_t k);
 int kth_dist_sample(kth_ctx *ctx, const int32_t *d_keys, int64_t n_local, uint32_t *d_sample,
                     int64_t s_local);

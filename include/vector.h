@@ -2,7 +2,7 @@
  * vector.h -- ABI twin of the reference's IntVector (vector.h:7-33).
  *
  * Same struct layout ({int size; int capacity; int *data;}, 16 bytes on LP64)
- * and the same 18 prototypes, so that the reference drivers
+ * and the same 17 prototypes, so that the reference drivers
  * (kth-problem-seq.c, TODO-kth-problem-cgm.c) compile and link unmodified
  * against libkth.so.  Implementation: mpi-k-selection_amd/csrc/vector.c.
  *

@@ -91,11 +91,11 @@ constexpr uint64_t DSCAN_PER_WG = 1ull << 16;  // candidates per workgroup of th
 struct kth_ctx {
     int device = 0;
     int main_grid[7] = {0, 0, 0, 0, 0, 0, 0};  // streaming-pass workgroups per k_main<TF> variant (KTH_MAIN_WG_PER_CU overrides)
-    bool fault_topk_rank = false;  // KTH_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
-    bool fault_barrier = false;    // KTH_FAULT_BARRIER (tests): k_finish reports a grid-barrier timeout
-    bool fault_once = false;       // KTH_FAULT_BARRIER=once: only the first cooperative launch does
+    bool fault_topk_rank = false;  // KTH_HOOK_FAULT_TOPK_RANK (tests): top-k selects a wrong rank on purpose
+    bool fault_barrier = false;    // KTH_HOOK_FAULT_BARRIER (tests): the grid barriers report a timeout
+    bool fault_once = false;       // (value 2) only the next cooperative launch does
     bool topk_stage = true;        // staged top-k (k_main<5/6>); KTH_TOPK_STAGE=0 turns it off
-    u64 topk_seg_cap = 0;          // KTH_TOPK_SEG_CAP (tests): entries per staging segment (0 = sized from n)
+    u64 topk_seg_cap = 0;          // KTH_HOOK_TOPK_SEG_CAP (tests): entries per staging segment (0 = sized from n)
     u64 sparse_per_wg = 0;  // keys per workgroup of the sparse levels (KTH_SPARSE_PER_WG; 0 = default)
     int post_dense_grid = POST_DENSE_GRID;    // decide level after the pass (KTH_POST_DENSE_GRID)
     int post_sparse_grid = LEVEL_GRID_MAX;    // candidate levels (KTH_POST_SPARSE_GRID)
@@ -727,15 +727,9 @@ int kth_ctx_create(int device, kth_ctx **out) {
             if (const char *g = getenv("KTH_FIN_GRID")) c->fin_grid = std::max(1, std::min(atoi(g), c->num_cu));
             if (const char *g = getenv("KTH_HEAD_SLACK")) c->head_slack64 = (uint32_t)std::max(0.0, atof(g) * 64.0);
             if (const char *g = getenv("KTH_HEAD_ABS")) c->head_abs_div = (uint32_t)std::max(0, atoi(g));
-            // test-only fault injection: kth_topk_i32 selects a neighbouring rank,
-            // so its count pass must report the bracket failure
-            c->fault_topk_rank = getenv("KTH_FAULT_TOPK_RANK") != nullptr;
-            if (const char *g = getenv("KTH_FAULT_BARRIER")) {
-                c->fault_barrier = true;
-                c->fault_once = !strcmp(g, "once");
-            }
             if (const char *g = getenv("KTH_TOPK_STAGE")) c->topk_stage = atoi(g) != 0;
-            if (const char *g = getenv("KTH_TOPK_SEG_CAP")) c->topk_seg_cap = (u64)std::max(0, atoi(g));
+            // (the fault injectors are not read from the environment: only
+            // kth_ctx_test_hook, which tests call explicitly, turns them on)
         }
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { rc = KTH_EHIP; break; }
         c->own_stream = true;
@@ -798,6 +792,23 @@ int kth_ctx_create(int device, kth_ctx **out) {
     }
     *out = c;
     return KTH_OK;
+}
+
+int kth_ctx_test_hook(kth_ctx *c, int hook, int64_t value) {
+    if (!c || value < 0) return KTH_EINVAL;
+    switch (hook) {
+    case KTH_HOOK_FAULT_TOPK_RANK: c->fault_topk_rank = value != 0; return KTH_OK;
+    case KTH_HOOK_FAULT_BARRIER:
+        if (value > 2) return KTH_EINVAL;
+        c->fault_barrier = value != 0;
+        c->fault_once = value == 2;
+        return KTH_OK;
+    case KTH_HOOK_TOPK_SEG_CAP:
+        if (value > (int64_t)1 << 40) return KTH_EINVAL;
+        c->topk_seg_cap = (u64)value;
+        return KTH_OK;
+    default: return KTH_EINVAL;
+    }
 }
 
 int kth_ctx_destroy(kth_ctx *c) {
@@ -1118,40 +1129,12 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         kth::k_topk_count<false, 0><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                             tcnt, tflags, head, nfull, sel_st, 0, rwl);
     }
-    if (getenv("KTH_TOPK_DEBUG")) {  // diagnostic: tile counts against a host recount
-        (void)hipStreamSynchronize(c->stream);
-        std::vector<uint32_t> h_t(ntiles), h_f(4), h_k(n);
-        std::vector<int32_t> h_v(2);
-        SelState h_s;
-        (void)hipMemcpy(h_t.data(), tcnt, ntiles * 4, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(h_f.data(), tflags, 16, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(h_v.data(), c->d_status, 8, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(&h_s, sel_st, sizeof h_s, hipMemcpyDeviceToHost);
-        (void)hipMemcpy(h_k.data(), d_keys, (size_t)n * 4, hipMemcpyDeviceToHost);
-        fprintf(stderr, "kth-topk-debug tf %d ncov %llu v %d err %d lo %d hi %d valid %u ovf %llu path %u\n", tf,
-                (unsigned long long)ncov, h_v[0], h_v[1], (int32_t)h_f[0], (int32_t)h_f[1], h_f[2],
-                (unsigned long long)h_s.cnt[4], h_s.path);
-        int shown = 0;
-        for (u64 t = 0; t < ntiles && shown < 8; ++t) {
-            uint32_t b = 0, e = 0;
-            for (u64 i = t * 1024; i < std::min<u64>((u64)n, t * 1024 + 1024); ++i) {
-                const int32_t x = (int32_t)h_k[i];
-                b += largest ? x > h_v[0] : x < h_v[0];
-                e += x == h_v[0];
-            }
-            if ((b | e << 16) != (h_t[t] & 0x7FFFFFFFu)) {
-                fprintf(stderr, "  tile %llu: got b %u e %u want b %u e %u\n", (unsigned long long)t, h_t[t] & 0xFFFF,
-                        h_t[t] >> 16, b, e);
-                ++shown;
-            }
-        }
-    }
     // tile offsets, block bases and need in one launch (a bracket failure --
     // counts that do not hold the k-th -- lands in the select's state, where
     // kth_ctx_last_stats reports it as .error)
     kth::k_topk_bases<<<(int)nblk, kth::TK_BLOCK, 0, c->stream>>>(
         tcnt, ntiles, toff, bsum, (u64)k, bbase, meta, c->st + c->last_state,
-        reinterpret_cast<uint32_t *>(c->islots + BAR_OFF) + kth::BAR_TAIL + 48);
+        reinterpret_cast<uint32_t *>(c->islots + BAR_OFF) + kth::BAR_TOPK_ARRIVE);
     if (tf >= 5) {
         auto tk5w = (u64)k * 32 <= (u64)n ? kth::k_tk5_write<kth::TK5_STAGE_SMALL> : kth::k_tk5_write<kth::TK5_STAGE_LARGE>;
         tk5w<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(

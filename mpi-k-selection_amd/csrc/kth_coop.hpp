@@ -34,7 +34,7 @@ struct CoopArgs {
     u64 zero2_words;
     uint32_t *tail;    // k_finish: FIN_LDS_KEYS keys of the last bin (finish_tail)
     uint32_t sample_ready;  // k_head: the sample (order keys) is already in `sample` (sharded window)
-    uint32_t fault;    // test hook (KTH_FAULT_BARRIER): the grid barriers report a timeout
+    uint32_t fault;    // test hook (KTH_HOOK_FAULT_BARRIER): the grid barriers and the tail wait report a timeout
     const uint32_t *pre;  // k_finish: k_main<0>'s first candidate digit (PreHist), or null
     uint32_t *pre_zero;   // k_finish: the other PreHist set, cleared for the next select
 };
@@ -341,7 +341,7 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
     // the others' keys are in once each has counted itself written (a
     // non-returning add after its stores are performed); the last to
     // reserve waits for that, bounded, and resets both words
-    uint32_t *written = x.bar + BAR_TAIL + 32;
+    uint32_t *written = x.bar + BAR_TAIL_WRITTEN;
     if (!s_last) {
         if (threadIdx.x == 0) __hip_atomic_fetch_add(written, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         KTH_STAMP(a, 5);
@@ -359,6 +359,10 @@ __device__ bool finish_tail(const StepArgs &a, SelState &ss, const CoopArgs &x, 
         }
         __hip_atomic_store(written, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next select
         __hip_atomic_store(ctl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x.fault) {  // test hook: as if this wait had timed out (the PreHist path has no grid barrier)
+            ss.error = ERR_BARRIER;
+            ss.mode = MODE_DONE;
+        }
     }
     __syncthreads();
     KTH_STAMP(a, 5);

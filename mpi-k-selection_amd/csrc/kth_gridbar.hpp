@@ -14,7 +14,11 @@ constexpr int BAR_NG = 64;           // group counters (workgroup w arrives on w
 constexpr int BAR_BASE = BAR_NG * BAR_GROUP_STRIDE;   // the groups' base values (BAR_NG words)
 constexpr int BAR_ERR = BAR_BASE + BAR_GROUP_STRIDE;
 constexpr int BAR_TAIL = BAR_ERR + BAR_GROUP_STRIDE;  // u64 at this u32 index: k_finish tail (arrivals << 32 | keys)
+constexpr int BAR_TAIL_WRITTEN = BAR_TAIL + 32;       // k_finish tail: workgroups whose keys are written
+constexpr int BAR_TOPK_ARRIVE = BAR_TAIL + 48;        // k_topk_bases: arrivals (zeroed by the last one)
 constexpr int BAR_WORDS = BAR_TAIL + BAR_GROUP_STRIDE;  // u32 words of barrier state per ctx
+static_assert(BAR_TAIL_WRITTEN >= BAR_TAIL + 2 && BAR_TOPK_ARRIVE > BAR_TAIL_WRITTEN && BAR_TOPK_ARRIVE < BAR_WORDS,
+              "the tail word (u64), its written count and the top-k arrival counter are distinct words");
 static_assert(BAR_NG <= WAVE && BAR_NG <= BAR_GROUP_STRIDE, "one wave polls every group; the bases fit one stride");
 constexpr uint32_t BAR_SPIN_LIMIT = 1u << 21;         // polls before a barrier gives up (seconds)
 constexpr uint32_t ERR_BARRIER = 64;

@@ -1764,9 +1764,9 @@ __global__ __launch_bounds__(BLOCK) void k_dlevel(StepArgs a) {
 // zeroes its share of the ctx-internal slots (16-byte stores).
 template <int BLOCK>
 // early (kth_dist_result_early: enqueued before the host knows how many levels
-// the protocol takes): every workgroup picks, and unless the pick finishes the
-// selection nothing is written or cleared -- the protocol then goes on and
-// its final k_dresult does the work.
+// the protocol takes): every workgroup picks, and while the picked state is
+// still live (more digits to come, no error) nothing is written or cleared --
+// the protocol then goes on and its final k_dresult does the work.
 __global__ __launch_bounds__(BLOCK) void k_dresult(StepArgs a, int32_t *d_out, int32_t *d_status, u64 *izero,
                                                    u64 izero_words, uint32_t early) {
     __shared__ SelState ss;
@@ -1775,7 +1775,10 @@ __global__ __launch_bounds__(BLOCK) void k_dresult(StepArgs a, int32_t *d_out, i
     if (blockIdx.x == 0 || early) {  // grid-uniform
         dist_state<BLOCK>(ss, a, cnts);
         dist_pick<BLOCK>(ss, a, scratch);
-        if (early && (ss.mode != MODE_DONE || ss.error)) return;  // block-uniform (the same pick in every block)
+        // early: leave only while the protocol goes on (a live state, no
+        // error); a finished state -- an answer or an error -- is written
+        // here, since kth_dist_result does not relaunch after one level
+        if (early && dist_live(ss) && !ss.error) return;  // block-uniform (the same pick in every block)
     }
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {

@@ -261,10 +261,13 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_bases(const uint32_t *__restr
         __hip_atomic_store(&bsum[2 * blockIdx.x], tot & 0xFFFFFFFFull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&bsum[2 * blockIdx.x + 1], tot >> 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wait_mem();
-        s_last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+        // release: this block's sums before its arrival; acquire: the last
+        // arrival sees every block's sums
+        s_last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
     }
     __syncthreads();
     if (!s_last) return;  // block-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (every thread of the last block reads the sums)
     // the last workgroup: exclusive bases of the block sums, need and the bracket check
     const int G = (int)gridDim.x, per = (G + TK_BLOCK - 1) / TK_BLOCK, g0 = threadIdx.x * per;
     u64 sb = 0, se = 0;

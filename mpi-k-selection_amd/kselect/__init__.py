@@ -29,6 +29,9 @@ from ._lib import (  # noqa: F401
     KTH_EINTERNAL,
     KTH_EINVAL,
     KTH_ENODEV,
+    KTH_HOOK_FAULT_BARRIER,
+    KTH_HOOK_FAULT_TOPK_RANK,
+    KTH_HOOK_TOPK_SEG_CAP,
     KTH_OK,
     KTH_PATH_LDS,
     KTH_PATH_RADIX,
@@ -159,6 +162,11 @@ class Selector:
         if r < 0:
             check(r, "kth_ctx_coop")
         return bool(r)
+
+    def test_hook(self, hook, value):
+        """TESTS ONLY: turn a fault injector of this ctx on or off
+        (kth_ctx_test_hook; KTH_HOOK_* in include/kth.h)."""
+        check(LIB.kth_ctx_test_hook(self._ctx, int(hook), int(value)), "kth_ctx_test_hook")
 
     def stats(self):
         st = KthStats()

@@ -25,6 +25,8 @@ KTH_DIST_DONE = 3  # kth_dist_level: no collective left, call kth_dist_result
 KTH_DIST_MAX_LEVELS = 3
 KTH_ROWS_MAX_COLS = 16384
 KTH_TOPK_MAX_COLS = 4096
+# kth_ctx_test_hook (tests only): fault injectors, off in every new ctx
+KTH_HOOK_FAULT_TOPK_RANK, KTH_HOOK_FAULT_BARRIER, KTH_HOOK_TOPK_SEG_CAP = 1, 2, 3
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -87,6 +89,7 @@ PROTOS = {
     "kth_select_i32_async": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, c_vp]),
     "kth_ctx_last_stats": (ctypes.c_int, [c_vp, ctypes.POINTER(KthStats)]),
     "kth_ctx_coop": (ctypes.c_int, [c_vp]),
+    "kth_ctx_test_hook": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int64]),
     "kth_ctx_enable_timing": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "kth_ctx_take_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]),

@@ -18,12 +18,18 @@ Replaces the CGM driver of the reference (TODO-kth-problem-cgm.c:76-278):
                                                  second (windows <= 2^24 values wide)
 
 Every rank ends with the same answer (the reference prints it on rank 0 only).
-The collectives never make the host wait between steps.  On GPUs they go
-through a direct RCCL communicator on the selector's own stream (kselect.rccl:
-torch's ProcessGroupNCCL would fence every collective with a hop to its
-internal stream); with gloo (CPU tests) they are torch.distributed ops.  The per-rank device work is a ``backend``:
-``HipBackend`` (libkth.so) in the product; tests plug in a CPU restatement to
-exercise this orchestration on gloo.
+On GPUs the collectives go through a direct RCCL communicator on the
+selector's own stream (kselect.rccl: torch's ProcessGroupNCCL would fence every
+collective with a hop to its internal stream), so enqueueing them never makes
+the host wait.  The host waits ONCE per selection: kth_dist_level(1) waits for
+level 0's kernel to learn from its DistStatus how many levels follow (by then
+the device has the second all-reduce, and with the early result the usual last
+step, queued behind it); the protocol is a loop over kth_dist_level until it
+returns KTH_DIST_DONE (at most KTH_DIST_MAX_LEVELS slots).  Ranks that share
+one GPU (KTH_SHARE_GPU=1, tests) stage the collectives through host memory over
+gloo (kselect.rccl.HostComm); CPU tests use torch.distributed ops directly.
+The per-rank device work is a ``backend``: ``HipBackend`` (libkth.so) in the
+product; tests plug in a CPU restatement to exercise this orchestration on gloo.
 """
 import os
 
@@ -32,7 +38,7 @@ import torch.distributed as dist
 
 from . import KTH_DIST_DONE, KTH_DIST_MAX_LEVELS, KTH_EINTERNAL, KTH_STATS_WORDS, LIB as _lib, KthError, Selector, check, \
     check_single_runtime
-from .rccl import RcclComm, TorchComm
+from .rccl import HostComm, RcclComm, TorchComm
 
 SMALL_PER_RANK = 64  # below this many keys per rank: all-gather and select locally
 
@@ -57,8 +63,11 @@ class HipBackend:
 
     def make_comm(self, group=None):
         """RCCL on this backend's stream for an "nccl" group (KTH_DIST_COMM=torch
-        forces torch.distributed collectives instead)."""
-        if dist.get_backend(group) == "nccl" and os.environ.get("KTH_DIST_COMM", "rccl") != "torch":
+        forces torch.distributed collectives instead); a CPU (gloo) group --
+        ranks sharing one GPU -- stages the device tensors through host memory."""
+        if dist.get_backend(group) != "nccl":
+            return HostComm(group)
+        if os.environ.get("KTH_DIST_COMM", "rccl") != "torch":
             return RcclComm(self.device.index, self.stream, group)
         return TorchComm(group)
 
@@ -213,11 +222,16 @@ class DistSelector:
             raise KthError(KTH_EINTERNAL, f"sharded select: device error {err}")
         return int(out.item())
 
+    def _coll_device(self):
+        """Where this group's own torch.distributed collectives take tensors:
+        host memory for a CPU (gloo) group, else the answer's device."""
+        return torch.device("cpu") if dist.get_backend(self.group) == "gloo" else self.out.device
+
     def _check_args(self, n_local, n_total, k, s_local):
         """Validate the arguments across ranks (two small collectives, once per
         distinct (n_local, n_total, k)), so that every rank raises together
         instead of one rank raising while the others wait in a collective."""
-        dev = self.out.device
+        dev = self._coll_device()
         mx = torch.tensor([n_total, -n_total, k, -k, 0 if n_local >= s_local else 1], dtype=torch.int64, device=dev)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
         tot = torch.tensor([n_local], dtype=torch.int64, device=dev)
@@ -238,18 +252,19 @@ class DistSelector:
     def _select_small(self, shard, n_local, n_total, k, out):
         """Tiny inputs (cf. the reference's final Gatherv + solve on one rank,
         TODO-kth-problem-cgm.c:235-278): all-gather the shards, select locally."""
-        sizes = [torch.zeros(1, dtype=torch.int64, device=self.out.device) for _ in range(self.world)]
-        dist.all_gather(sizes, torch.tensor([n_local], dtype=torch.int64, device=self.out.device), group=self.group)
+        dev = self._coll_device()
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
+        dist.all_gather(sizes, torch.tensor([n_local], dtype=torch.int64, device=dev), group=self.group)
         sizes = [int(x.item()) for x in sizes]
         if sum(sizes) != n_total:
             raise ValueError(f"shard sizes {sizes} do not sum to n_total={n_total}")
         m = max(sizes)
-        padded = torch.zeros(m, dtype=torch.int32, device=self.out.device)
+        padded = torch.zeros(m, dtype=torch.int32, device=dev)
         padded[:n_local] = shard[:n_local]
-        gathered = torch.empty(m * self.world, dtype=torch.int32, device=self.out.device)
+        gathered = torch.empty(m * self.world, dtype=torch.int32, device=dev)
         dist.all_gather_into_tensor(gathered, padded, group=self.group)
         union = torch.cat([gathered[r * m:r * m + sizes[r]] for r in range(self.world)])
-        self.b.select_all(union, n_total, k, out)
+        self.b.select_all(union.to(self.out.device), n_total, k, out)
         return out
 
     def close(self):

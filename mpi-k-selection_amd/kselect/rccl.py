@@ -112,6 +112,33 @@ class RcclComm:
             pass
 
 
+class HostComm:
+    """The two collectives of device tensors staged through host memory over a
+    CPU process group (gloo): device -> host copy (which waits for the stream's
+    work so far), the collective on host tensors, host -> device copy.  The
+    host waits at every collective; this is the transport of ranks that share
+    one GPU (bench.py / tests with KTH_SHARE_GPU=1, where RCCL refuses two ranks
+    on one device), the way apps/kth_cgm.c --comm mpi stages through MPI."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def all_reduce_sum_(self, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+        t.copy_(h)
+
+    def all_gather(self, out, inp):
+        h = inp.cpu()
+        o = torch.empty(out.numel(), dtype=out.dtype)
+        dist.all_gather_into_tensor(o, h, group=self.group)
+        out.copy_(o)
+
+    def close(self):
+        pass
+
+
 class TorchComm:
     """The same two collectives through torch.distributed (gloo tests, fallback)."""
 

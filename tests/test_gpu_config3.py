@@ -266,10 +266,9 @@ def test_lockstep_two_allreduces_p8(gpu, fam):
 
 
 def test_dist_error_surfaces(gpu):
-    """A grid-barrier timeout in the sharded window (KTH_FAULT_BARRIER) leaves
+    """A grid-barrier timeout in the sharded window (KTH_HOOK_FAULT_BARRIER) leaves
     the answer tensor unwritten, and DistSelector.error() reports it (the
     reused answer buffer must not pass for a fresh answer)."""
-    import os
     import torch
     import kselect
     from kselect.dist import DistSelector, HipBackend, lockstep
@@ -277,11 +276,8 @@ def test_dist_error_surfaces(gpu):
     t = torch.empty(n, dtype=torch.int32, device="cuda")
     gpu.fill(t, n, "uniform_full")
     gpu.sync()
-    os.environ["KTH_FAULT_BARRIER"] = "1"
-    try:
-        faulty = kselect.Selector(0)
-    finally:
-        del os.environ["KTH_FAULT_BARRIER"]
+    faulty = kselect.Selector(0)
+    faulty.test_hook(kselect.KTH_HOOK_FAULT_BARRIER, 1)
     try:
         ds = DistSelector(HipBackend(0, faulty), world=1)
         out = torch.full((1,), 12345, dtype=torch.int32, device="cuda")
@@ -290,3 +286,37 @@ def test_dist_error_surfaces(gpu):
         assert int(out.item()) == 12345
     finally:
         faulty.close()
+
+
+@pytest.mark.parametrize("early", ["1", "0"])
+def test_dist_level0_pick_error_surfaces(gpu, monkeypatch, early):
+    """Level 0's pick fails (the scan's all-reduced slot is tampered with: its
+    first-digit histogram zeroed, so no bin holds k) and level 0 was the last
+    level: with the early result on (KTH_DIST_EARLY=1, the default) its k_dresult
+    must write the error itself -- kth_dist_result does not relaunch after one
+    level -- so error() is nonzero and the answer tensor stays untouched; the
+    next select on the same ctx is exact again."""
+    import torch
+    from kselect import KTH_STATS_WORDS
+    from kselect.dist import DistSelector, HipBackend, lockstep
+    monkeypatch.setenv("KTH_DIST_EARLY", early)
+    n = (1 << 23) + 5
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu.fill(t, n, "uniform_full")
+    gpu.sync()
+    k = n // 2
+    want = int(torch.kthvalue(t.cpu(), k).values)
+    ds = DistSelector(HipBackend(0, gpu), world=1)
+    out = torch.full((1,), 12345, dtype=torch.int32, device="cuda")
+    ops = []
+    for op in ds.steps(t, n, n, k, out):  # world 1: the collectives are identities
+        ops.append(op[0])
+        if op[0] == "all_gather":
+            op[1].copy_(op[2])
+        elif ops.count("all_reduce") == 1:  # the scan's slot: counts kept, digit histogram zeroed
+            op[1][8:KTH_STATS_WORDS] = 0
+    assert ops == ["all_gather", "all_reduce", "all_reduce"], ops  # the error ends the protocol after level 0
+    assert ds.error() != 0
+    assert int(out.item()) == 12345
+    assert int(lockstep([ds], [t], [n], k, outs=[out])[0].item()) == want
+    assert ds.error() == 0

@@ -12,12 +12,11 @@
 * A cooperative window select followed by a sharded select on the SAME ctx: the
   window select leaves its count slot and candidate count for its next k_head
   to clear, so the sharded steps must clear them (kth_dist_begin).
-* Grid-barrier timeouts (KTH_FAULT_BARRIER): reported in the state, d_out left
+* Grid-barrier timeouts (the test-only KTH_HOOK_FAULT_BARRIER): reported in the state, d_out left
   untouched by the asynchronous entry, and the synchronous entry redoes the
   select on the per-level path.
 """
 import contextlib
-import os
 
 import numpy as np
 import pytest
@@ -134,26 +133,20 @@ def test_window_select_then_dist_on_same_ctx(gpu):
 @pytest.fixture
 def faulty():
     import kselect
-    os.environ["KTH_FAULT_BARRIER"] = "1"
-    try:
-        f = kselect.Selector(0)  # the hook is read when a ctx is created
-    finally:
-        del os.environ["KTH_FAULT_BARRIER"]
+    f = kselect.Selector(0)
+    f.test_hook(kselect.KTH_HOOK_FAULT_BARRIER, 1)
     yield f
     f.close()
 
 
 def test_coop_backoff_counts_every_entry_point(gpu):
-    """One grid-barrier timeout (KTH_FAULT_BARRIER=once) turns the cooperative
+    """One grid-barrier timeout (KTH_HOOK_FAULT_BARRIER, value 2: once) turns the cooperative
     kernels off for COOP_BACKOFF = 64 selections; asynchronous selects count
     down too, so a ctx used only asynchronously afterwards gets them back."""
     import torch
     import kselect
-    os.environ["KTH_FAULT_BARRIER"] = "once"
-    try:
-        sel = kselect.Selector(0)
-    finally:
-        del os.environ["KTH_FAULT_BARRIER"]
+    sel = kselect.Selector(0)
+    sel.test_hook(kselect.KTH_HOOK_FAULT_BARRIER, 2)
     try:
         n = (1 << 24) + 3
         keys, srt = _keys(gpu, n, "uniform_full")

@@ -155,16 +155,12 @@ def test_topk_tile_flag_cutoff_and_window_miss(gpu, largest):
 
 def test_topk_bracket_failure_is_reported(gpu):
     """A k-th that does not bracket k in the count pass (forced here with the
-    test-only KTH_FAULT_TOPK_RANK hook, which selects a neighbouring rank) must
+    test-only KTH_HOOK_FAULT_TOPK_RANK hook, which selects a neighbouring rank) must
     surface as kth_ctx_last_stats().error and leave the outputs unwritten."""
-    import os
     import torch
     import kselect
-    os.environ["KTH_FAULT_TOPK_RANK"] = "1"
-    try:
-        faulty = kselect.Selector(0)  # the hook is read when a ctx is created
-    finally:
-        del os.environ["KTH_FAULT_TOPK_RANK"]
+    faulty = kselect.Selector(0)
+    faulty.test_hook(kselect.KTH_HOOK_FAULT_TOPK_RANK, 1)
     n, k = (1 << 22) + 7, 1000
     a = np.random.default_rng(5).permutation(n).astype(np.int32)  # distinct keys
     d = torch.from_numpy(a).cuda()
@@ -245,17 +241,13 @@ def test_topk_staged_index_order(gpu, largest):
 
 
 def test_topk_staged_segment_overflow_falls_back(gpu):
-    """Staging segments too small for the kept side (KTH_TOPK_SEG_CAP, a
+    """Staging segments too small for the kept side (KTH_HOOK_TOPK_SEG_CAP, a
     test-only hook): the overflow flag sends the count and write passes back to
     the input, and the result is the same."""
-    import os
     import torch
     import kselect
-    os.environ["KTH_TOPK_SEG_CAP"] = "300"
-    try:
-        small = kselect.Selector(0)
-    finally:
-        del os.environ["KTH_TOPK_SEG_CAP"]
+    small = kselect.Selector(0)
+    small.test_hook(kselect.KTH_HOOK_TOPK_SEG_CAP, 300)
     n = (1 << 23) + 4099
     rng = np.random.default_rng(53)
     for name, a in _staged_cases(n, rng):
