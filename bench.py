@@ -224,7 +224,9 @@ def cpu_baseline_cgm(keys_np, procs, reps=3, timeout=120):
     """The reference CGM program (TODO-kth-problem-cgm.c compiled from its own
     source, n/k read from the environment: oracle/_ref/cgm_param) under
     `mpirun -n procs`; its own MPI_Wtime from before the Scatterv to the answer
-    (:76, :279).  Median of `reps` runs.  Raises on any failure."""
+    (:76, :279).  Median of `reps` runs; `wall_s` is the whole mpirun (rank 0's
+    key generation -- the input file read through the VecAdd shim -- included).
+    Raises on any failure."""
     import re
 
     import numpy as np
@@ -238,12 +240,14 @@ def cpu_baseline_cgm(keys_np, procs, reps=3, timeout=120):
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         keys_np.astype("<i4").tofile(f)
         path = f.name
-    times, answers = [], set()
+    times, answers, walls = [], set(), []
     try:
         env = dict(os.environ, KO_N=str(n), KO_K=str(n // 2), KO_TIME="1", KO_INPUT=path)
         for _ in range(reps):
+            w0 = time.monotonic()
             p = subprocess.run([mpirun, "-n", str(procs), binary], env=env, capture_output=True, text=True,
                                timeout=timeout, stdin=subprocess.DEVNULL)
+            walls.append(time.monotonic() - w0)
             m = re.search(r"kth element[= ]\s*(-?\d+)\s*\n\s*time:\s*([0-9.]+)", p.stdout)
             if not m:
                 raise RuntimeError(f"CGM baseline P={procs}: no answer line (rc {p.returncode}): "
@@ -256,7 +260,8 @@ def cpu_baseline_cgm(keys_np, procs, reps=3, timeout=120):
     return {"value": n / t / 1e9, "unit": "Gkeys/s", "cores": procs, "procs": procs, "kind": "reference",
             "sample": f"mpirun -n {procs} reference CGM (oracle/_ref/cgm_param) on 2^{n.bit_length() - 1} keys, "
                       f"k=n/2, median MPI_Wtime of {reps} runs {t * 1e3:.1f} ms (TODO-kth-problem-cgm.c:76,279)",
-            "seconds": t, "reps": reps, "answer": answers.pop() if len(answers) == 1 else sorted(answers)}
+            "seconds": t, "reps": reps, "n": n, "wall_s": float(np.median(walls)),
+            "answer": answers.pop() if len(answers) == 1 else sorted(answers)}
 
 
 def cpu_baselines(keys_np, family):
@@ -507,6 +512,8 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="global 1-based rank (default n_total/2)")
     ap.add_argument("--cpu-log2n", type=int, default=20, help="CPU baseline size (BASELINE config 1: 2^20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-full", action="store_true",
+                    help="skip the reference CGM leg at the GPU workload's own size (config 2: 2^30, ~45 s)")
     ap.add_argument("--local-shards", type=int, default=1,
                     help="P > 1: P shards of 2^log2n keys on this one GPU through kth_sharded_* (config 3 on one GPU)")
     ap.add_argument("--dist", action="store_true",
@@ -737,6 +744,25 @@ def main():
         res["cpu_baseline_cgm"] = cgm
         res["cpu_baseline_errors"] = errors
         res["cpu_host"] = host
+        if not args.no_cpu_full and P == 1 and args.log2n == 30:
+            # BASELINE config 2 "vs mpirun CGM on host cores" at config 2's own
+            # size, in this run: the reference CGM on the very keys the GPU
+            # selected (its answer must be the certified GPU answer)
+            share = min(CPU_SHARE, host["affinity_cpus"] or 1)
+            log(f"bench: reference CGM under mpirun -n {share} on the 2^30 GPU input (one run, ~45 s)")
+            try:
+                full = cpu_baseline_cgm(keys.cpu().numpy(), share, reps=1, timeout=600)
+                full["answer_ok"] = full["answer"] == v and bool(verified)
+                full["sample"] = (f"BASELINE config 2 at its own size: the reference CGM (oracle/_ref/cgm_param) under "
+                                  f"mpirun -n {share} (all cores of this job's CPU share) on the same 2^30 "
+                                  f"{args.family} keys the GPU selected, k=n/2, one run: MPI_Wtime "
+                                  f"{full['seconds']:.2f} s (TODO-kth-problem-cgm.c:76,279), {full['wall_s']:.1f} s "
+                                  f"wall with rank 0's key generation")
+                if not full["answer_ok"]:
+                    errors.append(f"CGM 2^30 P={share} answered {full['answer']}, the GPU's certified answer is {v}")
+                res["cpu_baseline_cgm_full"] = full
+            except Exception as e:  # noqa: BLE001 -- reported at the top level of the line
+                errors.append(f"CGM baseline 2^30 P={share}: {e!r}")
 
     if rank == 0:
         emit(res)

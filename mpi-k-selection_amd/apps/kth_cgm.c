@@ -10,9 +10,12 @@
  *   - MPI_Wtime from before the scatter to the answer (:76, :279) and rank 0's
  *     output lines: "kth element %d\n time: %f\n" (:289) when the answer is
  *     a window edge decided from the all-reduced counts (the reference's pivot
- *     found by its 3-way count, :194-201), else "kth element=%d \ntime: %f\n"
+ *     found by its 3-way count, :194-201; on the gather path for tiny inputs:
+ *     when every key equals the answer), else "kth element=%d \ntime: %f\n"
  *     (:280, the answer resolved from the candidates, as the reference's
- *     final gather + sort);
+ *     final gather + sort).  The reference's own choice is an artifact of its
+ *     pivot sequence (it depends on P); the two rules agree on every input
+ *     whose keys are all equal (:289) and differ elsewhere;
  *   - k is 1-based (VecGet(pVec, k - 1), :278).
  * Replaced: the local qsort (:115), the weighted-median rounds (:122-233) and
  * the final Gather/Gatherv + rank-0 sort (:235-278).  Each rank copies its shard
@@ -247,6 +250,9 @@ int main(int argc, char **argv)
         MPI_Gatherv(h_local, (int)n_local, MPI_INT, all, sizev, displs, MPI_INT, 0, MPI_COMM_WORLD);
         if (rank == 0) {
             KTHCHK(kth_select_i32_ctx(ctx, all, n, k, &answer));
+            /* one value: the select is decided by its counts (#< = 0, #== = n) */
+            by_counts = 1;
+            for (long long i = 0; i < n && by_counts; ++i) by_counts = all[i] == answer;
             free(all);
         }
         MPI_Bcast(&answer, 1, MPI_INT, 0, MPI_COMM_WORLD);

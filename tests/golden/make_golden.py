@@ -11,6 +11,10 @@ oracle/build_ref.sh compiles from it into oracle/_ref/).  Writes:
                   (libvector_ref.so: VecQuickSort + VecGet(k-1), kth-problem-seq.c:32-33)
       cgm_ref     {P: value | "livelock"} from `mpirun -n P cgm_param`
                   (TODO-kth-problem-cgm.c with n, k parameterised; timeout => livelock)
+      cgm_ref_line {P: 280 | 289 | "livelock"}: which of rank 0's two output
+                  lines the run printed -- "kth element=%d \ntime: %f\n" (:280,
+                  the final gather + sort) or "kth element %d\n time: %f\n" (:289,
+                  a weighted-median pivot that the 3-way count found, :194-201)
   and a "shipped" section: the unmodified reference programs run as shipped
   (n = 1e8), seeded through the --wrap=time shim, with their printed answers.
 
@@ -18,7 +22,9 @@ oracle/build_ref.sh compiles from it into oracle/_ref/).  Writes:
   BASELINE config 1), inputs regenerated from (family, seed, n) and pinned by
   sha256, expected outputs from the reference seq block and mpirun CGM.
 
-Usage: python tests/golden/make_golden.py [--small] [--shipped] [--large]
+Usage: python tests/golden/make_golden.py [--small] [--shipped] [--large] [--lines]
+(--lines: re-run the CGM reference on the recorded small and large cases and
+record only cgm_ref_line, checking that every value is reproduced)
 """
 import argparse
 import ctypes
@@ -68,6 +74,16 @@ def seq_ref(lib, a, k):
 
 
 _ANS = re.compile(r"kth element[= ]\s*(-?\d+)")
+_LINE_280 = re.compile(r"kth element=(-?\d+) \ntime: [0-9.]+\n")  # TODO-kth-problem-cgm.c:280
+_LINE_289 = re.compile(r"kth element (-?\d+)\n time: [0-9.]+\n")  # TODO-kth-problem-cgm.c:289
+
+
+def cgm_line(stdout):
+    """280 or 289: which of the reference's two answer lines rank 0 printed."""
+    a, b = _LINE_280.search(stdout), _LINE_289.search(stdout)
+    if bool(a) == bool(b):
+        raise RuntimeError(f"cgm output has {'both' if a else 'neither'} answer lines: {stdout!r}")
+    return 280 if a else 289
 
 
 def run_cgm(binary, P, env, timeout):
@@ -80,6 +96,12 @@ def run_cgm(binary, P, env, timeout):
     if not m:
         raise RuntimeError(f"cgm {binary} P={P}: no answer in {p.stdout!r} {p.stderr!r}")
     return int(m.group(1)), p.stdout
+
+
+def run_cgm_line(binary, P, env, timeout):
+    """(value, line) of one run; ("livelock", "livelock") on a timeout."""
+    val, out = run_cgm(binary, P, env, timeout)
+    return (val, "livelock") if out is None else (val, cgm_line(out))
 
 
 def ks_for(n):
@@ -99,12 +121,13 @@ def small(lib):
             srt = np.sort(a.astype(np.int64))
             for k in ks_for(n):
                 case = {"input": fname, "family": name, "n": n, "k": k,
-                        "true": int(srt[k - 1]), "seq_ref": seq_ref(lib, a, k), "cgm_ref": {}}
+                        "true": int(srt[k - 1]), "seq_ref": seq_ref(lib, a, k), "cgm_ref": {}, "cgm_ref_line": {}}
                 env = dict(os.environ, KO_N=str(n), KO_K=str(k), KO_TIME="1",
                            KO_INPUT=os.path.join(HERE, "inputs", fname))
                 for P in PS:
-                    val, _ = run_cgm(os.path.join(REF_DIR, "cgm_param"), P, env, CGM_TIMEOUT)
+                    val, line = run_cgm_line(os.path.join(REF_DIR, "cgm_param"), P, env, CGM_TIMEOUT)
                     case["cgm_ref"][str(P)] = val
+                    case["cgm_ref_line"][str(P)] = line
                 case["seq_ref_defect"] = case["seq_ref"] != case["true"]
                 cases.append(case)
                 print(name, n, k, case["true"], case["seq_ref"], case["cgm_ref"], flush=True)
@@ -126,8 +149,10 @@ def livelock_cases(lib):
             srt = np.sort(a.astype(np.int64))
             case = {"input": fname, "family": "uniform_full", "seed": seed, "n": n, "k": k,
                     "true": int(srt[k - 1]), "seq_ref": seq_ref(lib, a, k), "cgm_ref": {"2": val}}
+            case["cgm_ref_line"] = {"2": "livelock"}
             for P in (3, 4, 8):
-                case["cgm_ref"][str(P)], _ = run_cgm(os.path.join(REF_DIR, "cgm_param"), P, env, CGM_TIMEOUT)
+                case["cgm_ref"][str(P)], case["cgm_ref_line"][str(P)] = run_cgm_line(
+                    os.path.join(REF_DIR, "cgm_param"), P, env, CGM_TIMEOUT)
             case["seq_ref_defect"] = case["seq_ref"] != case["true"]
             out.append(case)
             print("livelock", seed, case, flush=True)
@@ -161,10 +186,11 @@ def large(lib):
             for k in sorted({1, n // 2, n}):
                 case = {"family": name, "dist": dist, "param": param, "seed": G.DEFAULT_SEED, "n": n, "k": k,
                         "input_sha256": sha256_file(path), "true": int(srt[k - 1]),
-                        "seq_ref": seq_ref(lib, a, k), "cgm_ref": {}}
+                        "seq_ref": seq_ref(lib, a, k), "cgm_ref": {}, "cgm_ref_line": {}}
                 env = dict(os.environ, KO_N=str(n), KO_K=str(k), KO_TIME="1", KO_INPUT=path)
                 for P in LARGE_PS:
-                    case["cgm_ref"][str(P)], _ = run_cgm(os.path.join(REF_DIR, "cgm_param"), P, env, 10.0)
+                    case["cgm_ref"][str(P)], case["cgm_ref_line"][str(P)] = run_cgm_line(
+                        os.path.join(REF_DIR, "cgm_param"), P, env, 10.0)
                 case["seq_ref_defect"] = case["seq_ref"] != case["true"]
                 out.append(case)
                 print("large", name, n, k, case["true"], case["seq_ref"], case["cgm_ref"], flush=True)
@@ -234,12 +260,49 @@ def shipped():
     return res
 
 
+def lines(doc):
+    """cgm_ref_line for every recorded small and large case, from fresh runs of
+    the same reference binary on the same inputs (each value must come out as
+    recorded: the runs are deterministic under KO_TIME)."""
+    tmp = tempfile.mkdtemp(prefix="ko_lines_")
+    for c in doc["cases"] + doc["large"]:
+        if "input" in c:
+            path = os.path.join(HERE, "inputs", c["input"])
+        else:
+            path = os.path.join(tmp, "in.bin")
+            G.gen(c["n"], c["dist"], c["seed"], c["param"]).astype("<i4").tofile(path)
+            assert sha256_file(path) == c["input_sha256"], c
+        env = dict(os.environ, KO_N=str(c["n"]), KO_K=str(c["k"]), KO_TIME="1", KO_INPUT=path)
+        c["cgm_ref_line"] = {}
+        for P, want in c["cgm_ref"].items():
+            if want == "livelock":  # (recorded as such; not re-run)
+                c["cgm_ref_line"][P] = "livelock"
+                continue
+            val, line = run_cgm_line(os.path.join(REF_DIR, "cgm_param"), int(P), env, 10.0 if "input" not in c else 5.0)
+            if val != want:
+                raise RuntimeError(f"cgm P={P} gave {val}, recorded {want}: {c}")
+            c["cgm_ref_line"][P] = line
+        print("lines", c.get("input", c["family"]), c["n"], c["k"], c["cgm_ref_line"], flush=True)
+    for f in os.listdir(tmp):
+        os.remove(os.path.join(tmp, f))
+    os.rmdir(tmp)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--shipped", action="store_true")
     ap.add_argument("--large", action="store_true")
+    ap.add_argument("--lines", action="store_true")
     args = ap.parse_args()
+    if args.lines:
+        path = os.path.join(HERE, "expected.json")
+        doc = json.load(open(path))
+        lines(doc)
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print("wrote", path)
+        return
     if not (args.small or args.shipped or args.large):
         args.small = args.shipped = args.large = True
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)

@@ -3,8 +3,16 @@
 two output lines with the true k-th smallest, which the golden fixtures pin to
 the reference's own mpirun answers: "kth element %d\n time: %f\n"
 (TODO-kth-problem-cgm.c:289, the reference's pivot found by its 3-way count)
-when the answer is a window edge decided from the all-reduced counts, else
+when the answer is a window edge decided from the all-reduced counts (on the
+gather path of tiny inputs: every key equals the answer), else
 "kth element=%d \ntime: %f\n" (:280, after the final gather + solve).
+
+Which line: the golden fixtures record the line the reference printed per case
+and P (cgm_ref_line).  The reference's choice follows its pivot sequence, so
+the two rules coincide only where the data decides both: inputs whose keys are
+all equal (:289 for every P).  There the driver's line must equal the
+reference's; everywhere its line must follow its own rule, restated
+independently by the CPU backend of the protocol (tests/dist_cpu_backend.py).
 
 CPU: the binary exists and fails loudly without a GPU (no CPU fallback).
 GPU: P = 1 (RCCL communicator) and P = 2 (two ranks share the one GPU, so the
@@ -17,7 +25,7 @@ import subprocess
 
 import pytest
 
-from conftest import GOLDEN, PKG
+from conftest import GOLDEN, PKG, load_input
 
 BIN = os.path.join(os.environ.get("KTH_BIN_DIR") or os.path.join(PKG, "bin"), "kth_cgm")
 MPIRUN = "/opt/conda/bin/mpirun"
@@ -57,7 +65,29 @@ def test_cgm_driver_fails_loudly_without_gpu():
 GOLDEN_SUBSET = {("uniform_full", 16384, "mid"), ("uniform_half", 16384, "mid"), ("uniform_ref", 16384, "mid"),
                  ("few_distinct", 16384, "mid"), ("all_equal", 16384, "mid"), ("sorted_desc", 16384, "mid"),
                  ("mod_1000", 16384, "mid"), ("uniform_full", 1000, "first"), ("uniform_full", 1000, "last"),
-                 ("sorted_asc", 16384, "mid")}
+                 ("sorted_asc", 16384, "mid"), ("all_equal", 7, "mid"), ("all_equal_min", 4093, "first"),
+                 ("all_equal_max", 4093, "last"), ("few_distinct", 1000, "mid")}
+
+
+def rule_line(a, k, P):
+    """The driver's documented line rule, restated on the CPU: :289 iff the
+    sharded protocol (P ranks, tests/dist_cpu_backend.py, slot-for-slot equal
+    to the device) ends with the answer on a window edge, decided from the
+    counts; on the gather path (n / P < 64) iff every key equals the answer."""
+    import numpy as np
+    import torch
+    from dist_cpu_backend import CpuBackend
+    from kselect.dist import SMALL_PER_RANK, DistSelector, lockstep, shard_bounds
+    n = a.size
+    if n // P < SMALL_PER_RANK:
+        return 289 if (a == np.sort(a)[k - 1]).all() else 280
+    sizes = [shard_bounds(n, r, P)[1] for r in range(P)]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    bs = [CpuBackend() for _ in range(P)]
+    out = lockstep([DistSelector(b, world=P) for b in bs], [t[offs[i]:offs[i + 1]] for i in range(P)], sizes, k)
+    key = (int(out[0][0]) & 0xFFFFFFFF) ^ 0x80000000
+    return 289 if bs[0].path == "window" and key in (bs[0].lo, bs[0].hi) else 280
 
 
 def _pick(c):
@@ -82,6 +112,10 @@ def test_cgm_driver_golden(golden, p):
         ref = c["cgm_ref"].get(str(max(p, 2)))
         if ref not in (None, "livelock"):
             assert got == ref, (c, p, got, ref)
+        a = load_input(c["input"])
+        assert line == rule_line(a, c["k"], p), (c, p, line)
+        if c["family"].startswith("all_equal"):  # where the two rules coincide: the reference's own line
+            assert line == c["cgm_ref_line"][str(max(p, 2))] == 289, (c, p, line)
         line_of[(c["family"], c["n"], {1: "first", c["n"]: "last"}.get(c["k"], "mid"))] = line
         seen += 1
     assert seen >= 8

@@ -59,6 +59,10 @@ def test_cgm_restatement_matches_reference(golden, oracle):
             else:
                 if st != 0 or out.value != ref:
                     mismatches.append((c["input"], c["k"], p, ref, st, out.value))
+                # the line the reference printed: :289 (found by a pivot's 3-way
+                # count, :194-201) or :280 (the final gather + sort)
+                if (289 if found.value else 280) != c["cgm_ref_line"][p]:
+                    mismatches.append((c["input"], c["k"], p, "line", c["cgm_ref_line"][p], found.value))
     assert not mismatches, mismatches[:10]
 
 
@@ -138,6 +142,8 @@ def test_large_fixtures_pin_the_restatement(golden, oracle):
                                    ctypes.byref(rounds), ctypes.byref(found))
             if (ref == "livelock" and st != 1) or (ref != "livelock" and (st != 0 or out.value != ref)):
                 mismatches.append((c["family"], c["n"], c["k"], p, ref, st, out.value))
+            if ref != "livelock" and (289 if found.value else 280) != c["cgm_ref_line"][p]:  # the printed line
+                mismatches.append((c["family"], c["n"], c["k"], p, "line", c["cgm_ref_line"][p], found.value))
     assert not mismatches, mismatches[:10]
     assert any(c["seq_ref_defect"] for c in large) and any(v == "livelock" for c in large
                                                           for v in c["cgm_ref"].values())
