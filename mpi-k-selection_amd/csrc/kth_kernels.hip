@@ -53,6 +53,7 @@ __device__ __forceinline__ uint4 load_nt(const uint4 *p) {
     const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(x.x, x.y, x.z, x.w);
 }
+__device__ __forceinline__ uint32_t load_nt(const uint32_t *p) { return __builtin_nontemporal_load(p); }
 
 struct StepArgs {
     const SelState *st_in;
@@ -978,26 +979,25 @@ struct OrdStager {
         __builtin_amdgcn_wave_barrier();
     }
 
-    // One wave-row slot: this lane's 4 consecutive keys q (positions p0 .. p0 + 3
-    // of the wave-row; key j valid iff bit j of valid4); stages the keys on the
-    // kept side of the far edge (x <= hi for TF 5, x >= lo for TF 6) in index
-    // order.  Returns the wave's count (wave-uniform).  When no lane stages two
-    // of its 4 keys (the usual case: ~1-2 % of the keys are staged), a key's
-    // slot is the fill plus mbcnt of the OR'ed ballots and the key is picked by
-    // selects on the ballots; otherwise a wave scan of the per-lane counts.
+    // One wave-row slot: this lane's keys q.x .. q.w at positions lane, 64 +
+    // lane, 128 + lane, 192 + lane of the wave-row (k_main<5/6> loads a
+    // wave-row as 4 dwords a lane, so that the order of the 4 ballots is the
+    // index order); stages the keys on the kept side of the far edge (x <= hi
+    // for TF 5, x >= lo for TF 6) in index order.  Returns the wave's count
+    // (wave-uniform).  Key j's slot is the fill plus the popcounts of ballots
+    // 0 .. j-1 plus its mbcnt in ballot j: no per-lane scan, whatever the
+    // density.  (Round 5 loaded 4 consecutive keys a lane, position 4 lane + j:
+    // a lane staging two of its keys -- most wave-rows at k = n / 16 -- then
+    // needed a wave scan of the per-lane counts, k_main<5> 994 us at k = 2^26.)
     // The keys equal to lo / hi are on the kept side too, so they are counted
     // here, behind the same wave-uniform test (ceqlo / ceqhi: this lane's).
     template <int TF>
-    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t valid4, uint32_t p0, uint32_t &ceqlo,
-                                            uint32_t &ceqhi) {
-        auto f1 = [&](uint32_t x, int j) {
-            return ((valid4 >> j) & 1u) != 0u && (TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo);
-        };
-        const bool c0 = f1(q.x, 0), c1 = f1(q.y, 1), c2 = f1(q.z, 2), c3 = f1(q.w, 3);
+    __device__ __forceinline__ uint32_t row(const uint4 &q, uint32_t lane, uint32_t &ceqlo, uint32_t &ceqhi) {
+        auto f1 = [&](uint32_t x) { return TF == 5 ? (int32_t)x <= shi : (int32_t)x >= slo; };
+        const bool c0 = f1(q.x), c1 = f1(q.y), c2 = f1(q.z), c3 = f1(q.w);
         const unsigned long long b0 = __builtin_amdgcn_ballot_w64(c0), b1 = __builtin_amdgcn_ballot_w64(c1),
                                  b2 = __builtin_amdgcn_ballot_w64(c2), b3 = __builtin_amdgcn_ballot_w64(c3);
-        const unsigned long long any = b0 | b1 | b2 | b3;
-        if (any == 0) return 0u;  // wave-uniform
+        if ((b0 | b1 | b2 | b3) == 0) return 0u;  // wave-uniform
         {
             const int32_t x0 = (int32_t)q.x, x1 = (int32_t)q.y, x2 = (int32_t)q.z, x3 = (int32_t)q.w;
             ceqlo += ((c0 & (x0 == slo)) ? 1u : 0u) + ((c1 & (x1 == slo)) ? 1u : 0u) +
@@ -1005,36 +1005,22 @@ struct OrdStager {
             ceqhi += ((c0 & (x0 == shi)) ? 1u : 0u) + ((c1 & (x1 == shi)) ? 1u : 0u) +
                      ((c2 & (x2 == shi)) ? 1u : 0u) + ((c3 & (x3 == shi)) ? 1u : 0u);
         }
-        const uint32_t total = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+        const uint32_t n0 = (uint32_t)__popcll(b0), n1 = (uint32_t)__popcll(b1), n2 = (uint32_t)__popcll(b2);
+        const uint32_t total = n0 + n1 + n2 + (uint32_t)__popcll(b3);
 #ifdef KTH_DIAG_TK5_NOSTAGE  // diagnostic builds only (wrong top-k results): cost of the staging
         return total;
 #endif
         if (wfill + total > CAP) flush();
         uint8_t *pb = reinterpret_cast<uint8_t *>(reg + CAP);
-        const unsigned long long coll = (b0 & b1) | ((b0 | b1) & b2) | ((b0 | b1 | b2) & b3);
-        if (coll == 0) {  // wave-uniform
-            const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, wfill));
-            // (selects in asm: as ?: the compiler may index the keys through scratch)
-            uint32_t val = q.x, j;
-            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.y), "s"(b1));
-            asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(j) : "s"(b1));
-            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.z), "s"(b2));
-            asm("v_cndmask_b32_e64 %0, %1, 2, %2" : "=v"(j) : "v"(j), "s"(b2));
-            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(val) : "v"(val), "v"(q.w), "s"(b3));
-            asm("v_cndmask_b32_e64 %0, %1, 3, %2" : "=v"(j) : "v"(j), "s"(b3));
-            if (c0 || c1 || c2 || c3) {
-                reg[at] = val;
-                pb[at] = (uint8_t)(p0 + j);
-            }
-        } else {
-            const uint32_t c = (c0 ? 1u : 0u) + (c1 ? 1u : 0u) + (c2 ? 1u : 0u) + (c3 ? 1u : 0u);
-            const uint32_t incl = wave_incl_scan32(c);
-            uint32_t at = wfill + incl - c;
-            if (c0) { reg[at] = q.x; pb[at] = (uint8_t)p0; ++at; }
-            if (c1) { reg[at] = q.y; pb[at] = (uint8_t)(p0 + 1); ++at; }
-            if (c2) { reg[at] = q.z; pb[at] = (uint8_t)(p0 + 2); ++at; }
-            if (c3) { reg[at] = q.w; pb[at] = (uint8_t)(p0 + 3); }
-        }
+        auto at = [](unsigned long long b, uint32_t base) {
+            return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, base));
+        };
+        const uint32_t a0 = at(b0, wfill), a1 = at(b1, wfill + n0), a2 = at(b2, wfill + n0 + n1),
+                       a3 = at(b3, wfill + n0 + n1 + n2);
+        if (c0) { reg[a0] = q.x; pb[a0] = (uint8_t)lane; }
+        if (c1) { reg[a1] = q.y; pb[a1] = (uint8_t)(WAVE + lane); }
+        if (c2) { reg[a2] = q.z; pb[a2] = (uint8_t)(2 * WAVE + lane); }
+        if (c3) { reg[a3] = q.w; pb[a3] = (uint8_t)(3 * WAVE + lane); }
         wfill += total;
         return total;
     }
@@ -1204,20 +1190,34 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     OrdStager os{region[wid], 0u, 0u, 0ull, ((u64)blockIdx.x * (BLK / WAVE) + wid) * seg.cap, slo, shi,
                  a.cand_count, a.stats_acc, a.cap, cand_out, seg};
     uint32_t clt = 0, ceqlo = 0, ceqhi = 0;  // per lane
-    // TF 5 / 6: the counts of 4 keys (as scan_keys) and their ordered staging
-    auto ord_keys = [&](const uint4 &q, uint32_t valid4, uint32_t p0) -> uint32_t {
+    // TF 5 / 6: the counts of one wave-row slot's 4 keys (as scan_keys) and
+    // their ordered staging (full tiles only)
+    auto ord_keys = [&](const uint4 &q) -> uint32_t {
 #ifdef KTH_DIAG_TK5_NOROW  // diagnostic builds only (wrong results): the pass without the staging compares
         clt += q.x < (uint32_t)slo;
         return 0u;
 #endif
-        const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
+        clt += ((int32_t)q.x < slo ? 1u : 0u) + ((int32_t)q.y < slo ? 1u : 0u) + ((int32_t)q.z < slo ? 1u : 0u) +
+               ((int32_t)q.w < slo ? 1u : 0u);
+        return os.template row<TF>(q, (uint32_t)lane, ceqlo, ceqhi);  // (the edges are counted there)
+    };
+    // TF 5 / 6 load a tile's wave-rows as dwords: row u of wave w is the 256
+    // keys u * 4 BLK + 256 w + [0, 256) (the same keys as the 16-byte loads'
+    // row u of the wave), lane l taking keys 64 j + l (j = 0..3) into x[u].
+    // Then the 4 ballots of a slot are in the wave-row's index order.  One
+    // load, a wait, then the rest, as load_tile.
+    auto load_tile_ord = [&](uint4 (&x)[U], u64 t) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(v + t * tile) + wid * (4 * WAVE) + lane;
+        x[0].x = load_nt(src);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        x[0].y = load_nt(src + WAVE);
+        x[0].z = load_nt(src + 2 * WAVE);
+        x[0].w = load_nt(src + 3 * WAVE);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int32_t x = (int32_t)k4[j];
-            const bool ok = (valid4 >> j) & 1u;
-            clt += (ok & (x < slo)) ? 1u : 0u;
+        for (int u = 1; u < U; ++u) {
+            const uint32_t *r = src + u * (4 * BLK);
+            x[u] = make_uint4(load_nt(r), load_nt(r + WAVE), load_nt(r + 2 * WAVE), load_nt(r + 3 * WAVE));
         }
-        return os.template row<TF>(q, valid4, p0, ceqlo, ceqhi);  // (the edges are counted there)
     };
 
     // a tile is consumed in groups of 4 * MAIN_SUB keys
@@ -1318,14 +1318,17 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
         uint4 x[U];
         RowAcc ra{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};
         const uint32_t e0 = ceqlo + ceqhi, c0 = clt;
-        load_tile(x, t);
+        if constexpr (ORD)
+            load_tile_ord(x, t);
+        else
+            load_tile(x, t);
         if constexpr (ORD) {
-            // row u: this lane's keys 4 * lane .. + 3 of the wave's 256 (its wave-row);
-            // lane u keeps row u's staged count for the row words
+            // row u: this lane's keys l, 64 + l, 128 + l, 192 + l of the wave's
+            // 256 (its wave-row); lane u keeps row u's staged count for the row words
             uint32_t rw = 0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t tot = ord_keys(x[u], 0xFu, 4u * (uint32_t)lane);
+                const uint32_t tot = ord_keys(x[u]);
                 rw = lane == u ? tot : rw;
             }
             tile_word = rw;
