@@ -24,7 +24,7 @@ def _rdv():
     return "file://" + os.path.join(tempfile.mkdtemp(prefix="kth_rdv_"), "store")
 
 
-def _worker(rank, world, rdv, cases, q):
+def _worker(rank, world, rdv, cases, q, host_comm=False):
     sys.path.insert(0, HERE)
     from conftest import PKG  # noqa: F401 -- sets sys.path for kselect and gen
     import torch
@@ -33,12 +33,15 @@ def _worker(rank, world, rdv, cases, q):
     import gen as G
     from dist_cpu_backend import CpuBackend
     from kselect.dist import DistSelector, shard_bounds
+    from kselect.rccl import HostComm
 
     dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         out = []
         for fam, param, n, ks, cap in cases:
-            ds = DistSelector(CpuBackend(cap=cap))
+            # host_comm: the shared-GPU transport (KTH_SHARE_GPU=1) -- its host
+            # staging is a copy here, its collectives the same gloo ops
+            ds = DistSelector(CpuBackend(cap=cap), comm=HostComm() if host_comm else None)
             start, cnt = shard_bounds(n, rank, world)
             shard = torch.from_numpy(G.gen(cnt, G.BY_NAME[fam], 0x5EED0001, param, offset=start, n_total=n))
             for k in ks:
@@ -50,11 +53,11 @@ def _worker(rank, world, rdv, cases, q):
         dist.destroy_process_group()
 
 
-def _run(world, cases):
+def _run(world, cases, host_comm=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     rdv = _rdv()
-    procs = [ctx.Process(target=_worker, args=(r, world, rdv, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, rdv, cases, q, host_comm)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -96,6 +99,21 @@ def test_dist_selector_gloo(world):
         for k in ks:
             answers = {by_rank[r][i][3] for r in range(world)}
             assert answers == {int(srt[k - 1])}, (fam, n, k, answers, int(srt[k - 1]))
+            i += 1
+
+
+def test_dist_selector_host_comm():
+    """DistSelector over kselect.rccl.HostComm (the transport of ranks sharing
+    one GPU, bench.py KTH_SHARE_GPU=1) at world 2: the same exact answers, the
+    small-input gather path included."""
+    cases = [(fam, param, n, sorted({1, n // 2, n}), cap) for fam, param, n, _, cap in
+             (CASES[0], CASES[2], CASES[4], CASES[6])]
+    res = _run(2, cases, host_comm=True)
+    i = 0
+    for fam, param, n, ks, _ in cases:
+        srt = _expected(fam, param, n)
+        for k in ks:
+            assert {res[r][i][3] for r in range(2)} == {int(srt[k - 1])}, (fam, n, k)
             i += 1
 
 
