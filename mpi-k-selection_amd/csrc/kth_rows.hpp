@@ -403,13 +403,41 @@ __device__ __forceinline__ uint32_t row_count_small(const uint32_t (&key)[KPL], 
 //   wider (clustered rows): the masked radix sweeps of the whole row
 //       (row_select_radix, rank kk_row in the row).
 // kk is the rank within bin B on entry and within the answer's equal keys on
-// return; key[] holds order keys (xor flip) on return.
-template <bool F32, int KPL, typename ToKeys>
+// return; key[] holds order keys (xor flip) on return when KEYS_OUT (else
+// float rows may keep raw bits).
+template <bool F32, int KPL, bool KEYS_OUT, typename ToKeys>
 __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], uint32_t *hist, int lane, uint32_t &kk,
                                                          uint32_t kk_row, uint32_t flip, bool vmap, float fs, float fo,
                                                          uint32_t bin, uint32_t cnt, uint32_t *eq_out,
                                                          ToKeys &&to_keys) {
     uint32_t amin = 0xFFFFFFFFu, amax = 0u;
+    if (F32 && vmap && vbin(-0.f, fs, fo) == bin && vbin(0.f, fs, fo) == bin) {  // wave-uniform
+        // bin B holds the value 0 (config 5's duplicate-heavy median: round(u *
+        // 8) / 8 puts 1/16 of a row on +-0).  When the row's zeros are exactly
+        // B's keys, their -0.0 / +0.0 counts decide: two compares a key counted
+        // on the scalar unit, no min / max pass over the bin, and k-th rows keep
+        // their raw bits (round 5 took the min / max pass, then these counts,
+        // then converted every key)
+        uint32_t cn = 0, cz = 0;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            cn += (uint32_t)__popcll(__ballot(key[j] == 0x80000000u));
+            cz += (uint32_t)__popcll(__ballot((key[j] << 1) == 0u));
+        }
+        if (cz == cnt) {  // wave-uniform: every key of B is a zero
+            const uint32_t kn = key_of_f32(0x80000000u) ^ flip, kp = key_of_f32(0u) ^ flip, cp = cz - cn;
+            const bool nfirst = kn < kp;  // the smaller order key first (flip: the k largest)
+            const uint32_t c1 = nfirst ? cn : cp, c2 = nfirst ? cp : cn;
+            if constexpr (KEYS_OUT) to_keys();
+            if (kk <= c1) {
+                if (eq_out) *eq_out = c1;
+                return nfirst ? kn : kp;
+            }
+            kk -= c1;
+            if (eq_out) *eq_out = c2;
+            return nfirst ? kp : kn;
+        }
+    }
     if (F32 && vmap) {  // key[] holds raw float bits
         const float s2 = opaque(fs);
         float o2;
@@ -638,8 +666,8 @@ __device__ __forceinline__ uint32_t row_select_fast(uint32_t (&key)[KPL], uint32
     __builtin_amdgcn_wave_barrier();  // every lane's histogram reads before the list overwrites it
     if (cnt > (uint32_t)WAVE) {
         kk -= below;
-        return row_select_dense_bin<F32, KPL>(key, hist, lane, kk, kk + below, flip, vmap, fs, fo, bin, cnt, eq_out,
-                                              to_keys);
+        return row_select_dense_bin<F32, KPL, KEYS_OUT>(key, hist, lane, kk, kk + below, flip, vmap, fs, fo, bin, cnt,
+                                                        eq_out, to_keys);
     }
     kk -= below;
 
