@@ -1140,12 +1140,15 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         tk5w<<<c->main_grid[tf] * TK5_SPLIT, kth::TK_BLOCK, 0, c->stream>>>(
             c->tk_segv, c->tk_segp, seg_cap, c->tk_wstart, nwin, (u64)c->main_grid[tf], tflags, nfull, c->d_status,
             flip, c->tk_wcnt, tcnt, toff, bbase, meta, d_vals, d_idx);
-        kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
+        kth::k_topk_write<true, true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip,
                                                                           tcnt, toff, bbase, meta, d_vals, d_idx,
                                                                           tflags, ncov);
-    } else
-        kth::k_topk_write<><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt, toff,
-                                                                bbase, meta, d_vals, d_idx);
+    } else if (aligned)
+        kth::k_topk_write<true><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                    toff, bbase, meta, d_vals, d_idx);
+    else
+        kth::k_topk_write<false><<<g, kth::TK_BLOCK, 0, c->stream>>>(keys, (u64)n, ntiles, c->d_status, flip, tcnt,
+                                                                     toff, bbase, meta, d_vals, d_idx);
     return launch_check();
 }
 

@@ -411,7 +411,7 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
                                                          uint32_t bin, uint32_t cnt, uint32_t *eq_out,
                                                          ToKeys &&to_keys) {
     uint32_t amin = 0xFFFFFFFFu, amax = 0u;
-    if (F32 && vmap && vbin(-0.f, fs, fo) == bin && vbin(0.f, fs, fo) == bin) {  // wave-uniform
+    if (F32 && !KEYS_OUT && vmap && vbin(-0.f, fs, fo) == bin && vbin(0.f, fs, fo) == bin) {  // wave-uniform
         // bin B holds the value 0 (config 5's duplicate-heavy median: round(u *
         // 8) / 8 puts 1/16 of a row on +-0).  When the row's zeros are exactly
         // B's keys, their -0.0 / +0.0 counts decide: two compares a key counted
@@ -423,6 +423,7 @@ __device__ __forceinline__ uint32_t row_select_dense_bin(uint32_t (&key)[KPL], u
         for (int j = 0; j < KPL; ++j) {
             cn += (uint32_t)__popcll(__ballot(key[j] == 0x80000000u));
             cz += (uint32_t)__popcll(__ballot((key[j] << 1) == 0u));
+            if (j % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // (the masks die at once: no SGPR build-up)
         }
         if (cz == cnt) {  // wave-uniform: every key of B is a zero
             const uint32_t kn = key_of_f32(0x80000000u) ^ flip, kp = key_of_f32(0u) ^ flip, cp = cz - cn;

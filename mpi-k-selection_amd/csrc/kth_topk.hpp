@@ -296,32 +296,24 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_bases(const uint32_t *__restr
 }
 
 // Pass 5: ordered compaction.  Each wave looks at 64 tiles at once (one per
-// lane, for the bookkeeping) and visits only those holding output keys.  A
-// tile is read as 16 dwords a lane: x[j] of lane l is key 64 j + l of the
-// tile, so the wave's j-th load is 64 consecutive keys and its ballots are in
-// index order.  A kept key's slot in its tile's output range -- which is
-// contiguous, [bb + min(be, need), + #better + #kept ties) -- is then
-//   r = pb + min(pe, cap),
-// pb / pe the better / equal keys of the tile before it (the loads before:
-// wave-uniform running counts; this load: mbcnt of its ballot) and cap =
-// clamp(need - be, 0, 65535) the ties the tile may still take; a tie is kept
-// when pe < cap.  Each load's kept keys are one contiguous run of slots and go
-// straight from registers to the outputs: no LDS staging, no wave scan, no
-// copy-out loop.  Ties (keys equal to the k-th: one value) are rare, so their
-// mbcnt runs only under a ballot that has one.  (Round 5 read 16 consecutive
-// keys a lane as four 16-byte loads, placed the kept ones in the wave's LDS
-// through a wave scan of per-lane counts and copied them out coalesced: 108-138
-// VGPRs, 3 waves a SIMD, and a wave waited for its copy-out stores whenever it
-// waited for its next loads (one memory counter): 1264 us at k = 2^27 and 2264
-// us at k = 2^29, ~4.7 TB/s of its read + write bytes.)
+// lane) and visits only those holding output keys.  Lane l owns keys
+// [1024 t + 16 l, +16) of tile t, so a wave scan of the per-lane counts gives
+// every kept key its slot in the tile's output range, which is contiguous:
+// [bb + min(be, need), + #better + #kept ties).  Inside the range a key's
+// slot is 32-bit arithmetic: with pb / pe the better / equal keys of the tile
+// before it and cap = clamp(need - be, 0, 65535) the ties the tile may still
+// take, a better key goes to pb + min(pe, cap), a tie with pe < cap to pb + pe.
+// The pairs are staged in the wave's LDS and written out coalesced.
+// Measured (rocprof averages, k = 2^27 / 2^29): nontemporal key loads 1436 /
+// 2336 us against plain loads 1251 / 1934 (one box); four tiles a round
+// against two 1261 / 2251 against 1304 / 2275 (another box).  Also measured
+// and dropped there: nontemporal output stores (1433 / 2952) and issuing the
+// next round's loads before placing this one (142 VGPRs; 1284 / 2279).
 #ifndef KTH_TKW_TILES
-#define KTH_TKW_TILES 2
-#endif
-#ifndef KTH_TKW_STRIDED
-#define KTH_TKW_STRIDED 1
+#define KTH_TKW_TILES 4
 #endif
 constexpr int TKW_TILES = KTH_TKW_TILES;  // tiles a wave loads together in k_topk_write
-template <bool STAGED = false>
+template <bool ALIGNED, bool STAGED = false>
 __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restrict__ keys, u64 n, u64 ntiles,
                                                          const int32_t *__restrict__ d_v, uint32_t flip,
                                                          const uint32_t *__restrict__ tcnt,
@@ -329,26 +321,52 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
                                                          const u64 *__restrict__ meta, int32_t *__restrict__ vals,
                                                          int64_t *__restrict__ idx,
                                                          const uint32_t *__restrict__ tflags = nullptr, u64 ncov = 0) {
+    __shared__ uint32_t s_val[TK_BLOCK / WAVE][TK_TILE];
+    __shared__ uint16_t s_col[TK_BLOCK / WAVE][TK_TILE];
     if (meta[1]) return;
     const u64 need = meta[0];
-    const int32_t v = d_v[0];
+    const uint32_t uv = key_of_i32((uint32_t)d_v[0]);
     const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const u64 nw = (u64)gridDim.x * (TK_BLOCK / WAVE);
     const u64 t_from = STAGED && tk5_ok(tflags, d_v) ? ncov : 0;  // tiles below t_from: k_tk5_write
-#if KTH_TKW_STRIDED
-    // wave gw takes tiles g0 + gw + l nw (l = 0..63) of each group of 64 nw
-    // tiles: all waves walk the input together, one window of nw tiles at a
-    // time (DRAM rows stay open), instead of each wave its own 64 tiles
-    const u64 gw = (u64)blockIdx.x * (TK_BLOCK / WAVE) + w, ts = nw;
-    for (u64 tg = gw; tg < ntiles; tg += WAVE * nw) {
-        if (tg + (WAVE - 1) * ts < t_from) continue;  // wave-uniform
-#else
-    const u64 ts = 1;
+    // one round: up to TKW_TILES tiles of the wave's 64 (the next set bits of todo)
+    struct Round {
+        int src[TKW_TILES];  // lane (tile - tg) of each tile, -1 past the last
+        uint32_t x[TKW_TILES][TK_KPL];
+    };
+    auto load_round = [&](Round &rd, u64 &todo, u64 tg) {
+#pragma unroll
+        for (int q = 0; q < TKW_TILES; ++q) {
+            const bool has = todo != 0;  // wave-uniform
+            rd.src[q] = has ? __builtin_ctzll(todo) : -1;
+            if (has) todo &= todo - 1;
+            const u64 tb = (tg + (u64)(has ? rd.src[q] : 0)) * TK_TILE;
+            if (!has) {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) rd.x[q][j] = 0u;
+            } else if (ALIGNED && tb + TK_TILE <= n) {
+#pragma unroll
+                for (int r = 0; r < TK_KPL / 4; ++r) {
+                    const uint4 *p4 = reinterpret_cast<const uint4 *>(keys + tb + (u64)lane * TK_KPL + 4 * r);
+                    const uint4 v4 = *p4;
+                    rd.x[q][4 * r] = v4.x;
+                    rd.x[q][4 * r + 1] = v4.y;
+                    rd.x[q][4 * r + 2] = v4.z;
+                    rd.x[q][4 * r + 3] = v4.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < TK_KPL; ++j) {
+                    const u64 i = tb + (u64)lane * TK_KPL + j;
+                    rd.x[q][j] = i < n ? keys[i] : 0u;
+                }
+            }
+        }
+    };
     for (u64 tg = ((u64)blockIdx.x * (TK_BLOCK / WAVE) + w) * WAVE; tg < ntiles; tg += nw * WAVE) {
         if (tg + WAVE <= t_from) continue;  // wave-uniform
-#endif
-        // lane l: tile tg + l ts's bases and whether it holds output keys
-        const u64 tl = tg + lane * ts;
+        // lane l: tile tg + l's bases and whether it holds output keys
+        const u64 tl = tg + lane;
         uint32_t c_l = 0;
         u64 bb_l = 0, be_l = 0;
         if (tl < ntiles) {
@@ -359,65 +377,60 @@ __global__ __launch_bounds__(TK_BLOCK) void k_topk_write(const uint32_t *__restr
         }
         const bool act = tl >= t_from && (tk_better_of(c_l) != 0 || (tk_equal_of(c_l) != 0 && be_l < need));
         u64 todo = __ballot(act);
-        while (todo) {  // TKW_TILES tiles a round, their loads in flight together
-            int src[TKW_TILES];  // lane (tile - tg) of each tile, -1 past the last
-            uint32_t x[TKW_TILES][TK_KPL];
+        // TKW_TILES tiles a round, all their loads in flight together (one
+        // tile's 4 KiB a wave left the loads idle while the tile was placed
+        // and copied out: k = 2^27 1398 -> 1346 us on one box, ~equal on
+        // another).  (A layout in which each load instruction reads 1 KiB
+        // contiguous, four wave scans a tile, measured no faster: 1377 vs
+        // 1347 us at 2^27, 2339 vs 2322 at 2^29.)
+        while (todo) {
+            Round cur;
+            load_round(cur, todo, tg);
 #pragma unroll
             for (int q = 0; q < TKW_TILES; ++q) {
-                const bool has = todo != 0;  // wave-uniform
-                src[q] = has ? __builtin_ctzll(todo) : -1;
-                if (has) todo &= todo - 1;
-                const u64 tb = (tg + (u64)(has ? src[q] : 0) * ts) * TK_TILE;
-                const uint32_t *p = keys + tb + lane;
-                if (has && tb + TK_TILE <= n) {
-#pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = p[j * WAVE];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < TK_KPL; ++j) x[q][j] = has && tb + (u64)(j * WAVE + lane) < n ? p[j * WAVE] : 0u;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < TKW_TILES; ++q) {
-                const int sq = src[q];
-                if (sq < 0) break;  // wave-uniform
-                const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), sq) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, sq);
-                const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), sq) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, sq);
-                const u64 room = be >= need ? 0 : need - be;                // ties this tile may take
+                const int src = cur.src[q];
+                if (src < 0) break;  // wave-uniform
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)c_l, src);
+                const u64 bb = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bb_l >> 32), src) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bb_l, src);
+                const u64 be = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(be_l >> 32), src) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)be_l, src);
+                const u64 ce = tk_equal_of(c);
+                const u64 room = be >= need ? 0 : need - be;               // ties this tile may take
                 const uint32_t cap = (uint32_t)(room < 0xFFFFu ? room : 0xFFFFu);
-                const u64 start = bb + (be < need ? be : need);             // the tile's first output slot
-                const u64 tb = (tg + (u64)sq * ts) * TK_TILE;
-                int32_t *const vo = vals ? vals + start : nullptr;
-                int64_t *const io = idx ? idx + start : nullptr;
-                const bool full = tb + TK_TILE <= n;
-                uint32_t pb = 0, pe = 0;  // wave-uniform: better / equal keys of the tile so far
+                const uint32_t total = tk_better_of(c) + (uint32_t)(room < ce ? room : ce);  // output keys
+                const u64 start = bb + (be < need ? be : need);             // and where they go
+                const u64 tb = (tg + (u64)src) * TK_TILE;
+                uint32_t mb = 0, me = 0;  // bit j: this lane's key j is better / equal
 #pragma unroll
                 for (int j = 0; j < TK_KPL; ++j) {
-                    const uint32_t i = (uint32_t)(j * WAVE + lane);  // the key's index in its tile
-                    const bool in = full || tb + i < n;
-                    const int32_t xk = (int32_t)x[q][j];
-                    const bool isb = in && (flip == 0u ? xk < v : xk > v), ise = in && xk == v;
-                    const u64 Bb = __ballot(isb), Be = __ballot(ise);
-                    if ((Bb | Be) == 0) continue;  // wave-uniform
-                    uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(Bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Bb, pb));
-                    bool keep = isb;
-                    if (Be == 0) {  // wave-uniform: no tie in this load (the usual case)
-                        r += min(pe, cap);
-                    } else {
-                        const uint32_t re =
-                            __builtin_amdgcn_mbcnt_hi((uint32_t)(Be >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Be, pe));
-                        r += min(re, cap);
-                        keep = isb || (ise && re < cap);
-                    }
-                    if (keep) {
-                        if (vo) vo[r] = xk;
-                        if (io) io[r] = (int64_t)(tb + i);
-                    }
-                    pb += (uint32_t)__popcll(Bb);
-                    pe += (uint32_t)__popcll(Be);
+                    const bool in = tb + TK_TILE <= n || tb + (u64)lane * TK_KPL + j < n;
+                    const uint32_t u = key_of_i32(cur.x[q][j]);
+                    mb |= (uint32_t)(in && tk_better(u, uv, flip)) << j;
+                    me |= (uint32_t)(in && u == uv) << j;
                 }
+                const uint32_t mine = (uint32_t)__popc(mb) | ((uint32_t)__popc(me) << 16);
+                const uint32_t p = wave_incl_scan32(mine) - mine;
+                if (mb | me) {
+                    uint32_t pb = p & 0xFFFFu, pe = p >> 16;
+#pragma unroll
+                    for (int j = 0; j < TK_KPL; ++j) {
+                        const uint32_t isb = (mb >> j) & 1u, ise = (me >> j) & 1u;
+                        const uint32_t r = pb + min(pe, cap);
+                        if (isb | (ise & (uint32_t)(pe < cap))) {
+                            s_val[w][r] = cur.x[q][j];
+                            s_col[w][r] = (uint16_t)(lane * TK_KPL + j);
+                        }
+                        pb += isb;
+                        pe += ise;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t r = lane; r < total; r += WAVE) {  // coalesced copy-out
+                    if (vals) vals[start + r] = (int32_t)s_val[w][r];
+                    if (idx) idx[start + r] = (int64_t)(tb + s_col[w][r]);
+                }
+                __builtin_amdgcn_wave_barrier();  // copy-out reads before the next tile's staging
             }
         }
     }
