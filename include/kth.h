@@ -233,6 +233,21 @@ int kth_dist_result(kth_ctx *ctx, int32_t *d_out);
  * kth_dist_result with the same d_out is then the only launch that writes (and
  * costs nothing when the early one finished the select). */
 int kth_dist_result_early(kth_ctx *ctx, int32_t *d_out);
+/* The whole step sequence above in ONE call, for a caller that holds an RCCL
+ * communicator (one process per GPU): kth_dist_begin .. kth_dist_result with
+ * the all-gather of the samples and the slot all-reduces as ncclAllGather /
+ * ncclAllReduce (uint64 SUM) on the ctx stream, the early result before
+ * level 1 when `early` is nonzero.  nccl_all_reduce / nccl_all_gather are the
+ * caller's ncclAllReduce / ncclAllGather entry points, so that the
+ * communicator `nccl_comm` (an ncclComm_t of `world` ranks) and the calls come
+ * from one RCCL copy.  d_sample: s_local uint32 words, d_gathered: world *
+ * s_local; every rank passes the same (n_total, k, s_local).  The host waits
+ * once, for level 0's status, as in the step sequence; the answer lands in
+ * *d_out (device).  Replaces the per-step host round trips of a scripted
+ * caller (kselect.dist uses it over RCCL). */
+int kth_dist_select_rccl(kth_ctx *ctx, void *nccl_all_reduce, void *nccl_all_gather, void *nccl_comm, int world,
+                         const int32_t *d_keys, int64_t n_local, int64_t n_total, int64_t k, uint64_t *d_slots,
+                         uint32_t *d_sample, uint32_t *d_gathered, int64_t s_local, int32_t *d_out, int early);
 /* Sample size for n keys (the single-GPU rule: min(2^20, n/64), a multiple
  * of 64).  Sharded callers take about kth_dist_sample_size(n_total) / P keys
  * per rank (a multiple of 64, at least 64), so that the all-gathered sample

@@ -1364,6 +1364,8 @@ int kth_internal_slots_sum(uint64_t *const *slots, int P, int slot, void *stream
     return launch_check();
 }
 
+void *kth_internal_ctx_stream(const kth_ctx *c) { return c ? reinterpret_cast<void *>(c->stream) : nullptr; }
+
 int kth_internal_status_gather(kth_ctx *const *ctxs, int P, int32_t *d_dst, void *stream) {
     if (!ctxs || !d_dst || P < 1 || P > KTH_LOCAL_MAX_SHARDS) return KTH_EINVAL;
     kth::StatusPtrs p{};

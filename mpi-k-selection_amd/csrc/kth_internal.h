@@ -37,6 +37,9 @@ __attribute__((visibility("hidden"))) int kth_internal_dist_window_share(struct 
 __attribute__((visibility("hidden"))) int kth_internal_status_gather(struct kth_ctx *const *ctxs, int P,
                                                                      int32_t *d_dst, void *stream);
 
+/* The ctx's stream (its own, or the one kth_ctx_set_stream gave it). */
+__attribute__((visibility("hidden"))) void *kth_internal_ctx_stream(const struct kth_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif

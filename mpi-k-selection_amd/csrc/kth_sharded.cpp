@@ -469,3 +469,47 @@ int kth_select_i32_sharded(const int32_t *const *dev_shards, const int64_t *shar
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// One sharded selection over the caller's RCCL communicator, one call: the
+// kth_dist_* steps of this rank with the collectives in between, all on the
+// ctx stream.  A scripted caller (kselect.dist) paid one host round trip per
+// step through its bindings -- ~18 us of device idle a select at world size
+// 1, the host's path from its wait on level 0 to the next select's first
+// launch (profiles/r5_dist_early_result.txt) -- which this call removes.
+extern "C" int kth_dist_select_rccl(kth_ctx *ctx, void *nccl_all_reduce, void *nccl_all_gather, void *nccl_comm,
+                                    int world, const int32_t *d_keys, int64_t n_local, int64_t n_total, int64_t k,
+                                    uint64_t *d_slots, uint32_t *d_sample, uint32_t *d_gathered, int64_t s_local,
+                                    int32_t *d_out, int early) {
+    using AllReduceFn = ncclResult_t (*)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                         hipStream_t);
+    using AllGatherFn = ncclResult_t (*)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    if (!ctx || !nccl_all_reduce || !nccl_all_gather || !nccl_comm || world < 1 || !d_keys || !d_slots ||
+        !d_sample || !d_gathered || !d_out || s_local < 64)
+        return KTH_EINVAL;
+    const auto all_reduce = reinterpret_cast<AllReduceFn>(nccl_all_reduce);
+    const auto all_gather = reinterpret_cast<AllGatherFn>(nccl_all_gather);
+    const auto comm = reinterpret_cast<ncclComm_t>(nccl_comm);
+    const auto stream = reinterpret_cast<hipStream_t>(kth_internal_ctx_stream(ctx));
+    auto reduce = [&](int slot) -> int {
+        uint64_t *p = d_slots + (size_t)slot * KTH_STATS_WORDS;
+        NCCLT(all_reduce(p, p, KTH_STATS_WORDS, ncclUint64, ncclSum, comm, stream));
+        return KTH_OK;
+    };
+    TRY(kth_dist_begin(ctx, d_slots, n_total, k));
+    TRY(kth_dist_sample(ctx, d_keys, n_local, d_sample, s_local));
+    NCCLT(all_gather(d_sample, d_gathered, (size_t)s_local, ncclUint32, comm, stream));
+    TRY(kth_dist_window(ctx, d_gathered, s_local * world));
+    int slot = kth_dist_scan(ctx, d_keys, n_local);
+    TRY(slot);
+    TRY(reduce(slot));
+    for (int l = 0;; ++l) {  // usually one level: two all-reduces in all
+        if (l > KTH_DIST_MAX_LEVELS) return KTH_EINTERNAL;
+        if (l == 1 && early) TRY(kth_dist_result_early(ctx, d_out));  // before level 1 waits for level 0
+        slot = kth_dist_level(ctx, d_keys, n_local, l);
+        TRY(slot);
+        if (slot == KTH_DIST_DONE) break;
+        TRY(reduce(slot));
+    }
+    return kth_dist_result(ctx, d_out);
+}

@@ -109,6 +109,8 @@ PROTOS = {
     "kth_dist_level": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int]),
     "kth_dist_result": (ctypes.c_int, [c_vp, c_vp]),
     "kth_dist_result_early": (ctypes.c_int, [c_vp, c_vp]),
+    "kth_dist_select_rccl": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_int64, c_vp, c_vp, c_vp, ctypes.c_int64, c_vp, ctypes.c_int]),
     "kth_dist_sample_size": (ctypes.c_int64, [ctypes.c_int64]),
     "kth_sample_chunk": (ctypes.c_int, []),
     "kth_window_z": (ctypes.c_double, []),

@@ -105,6 +105,15 @@ class HipBackend:
     def result(self, out):
         check(_lib.kth_dist_result(self.ctx, out.data_ptr()), "kth_dist_result")
 
+    def select_rccl(self, comm, shard, n_local, n_total, k, slots, sample, gathered, s_local, out, early):
+        """The whole protocol in one call over an RcclComm (kth_dist_select_rccl)."""
+        c, ar, ag = comm.entry_points()
+        r = _lib.kth_dist_select_rccl(self.ctx, ar, ag, c, comm.world, shard.data_ptr(), n_local, n_total, k,
+                                      slots.data_ptr(), sample.data_ptr(), gathered.data_ptr(), s_local,
+                                      out.data_ptr(), early)
+        if r:
+            check(r, "kth_dist_select_rccl")
+
     def result_early(self, out):
         """The result enqueued before level 1 looks at level 0's status (a
         no-op on the device unless level 0 was the last); result() closes."""
@@ -138,6 +147,7 @@ class DistSelector:
         self._gathered = None
         self._checked = None  # last (n_local, n_total, k) every rank agreed on
         self._s_local_for, self._s_local, self._sample_n = None, 0, -1
+        self._one_call, self._early = None, 1  # (decided at the first select)
 
     def s_local(self, n_total):
         """Sample keys per rank: the window needs ~sample_size(n_total) keys in
@@ -201,6 +211,22 @@ class DistSelector:
             return self._select_small(shard, n_local, n_total, k, out)
         if self._checked != (n_local, n_total, k):
             self._check_args(n_local, n_total, k, self.s_local(n_total))
+        if self._one_call is None:
+            # over RCCL: every step and collective in one library call (the
+            # host's per-step round trips through the bindings are ~35 us a
+            # select); KTH_DIST_PY=1 keeps the scripted steps
+            self._one_call = (isinstance(self.comm, RcclComm) and hasattr(self.b, "select_rccl")
+                              and os.environ.get("KTH_DIST_PY") != "1")
+            self._early = 1 if os.environ.get("KTH_DIST_EARLY", "1") != "0" else 0
+        if self._one_call:
+            s_local = self.s_local(n_total)
+            if self._sample_n != s_local:
+                self._sample = self.b.alloc_sample(s_local)
+                self._gathered = self.b.alloc_sample(s_local * self.world)
+                self._sample_n = s_local
+            self.b.select_rccl(self.comm, shard, n_local, n_total, k, self.slots, self._sample, self._gathered,
+                               s_local, out, self._early)
+            return out
         for op in self.steps(shard, n_local, n_total, k, out):
             if op[0] == "all_gather":
                 self.comm.all_gather(op[1], op[2])

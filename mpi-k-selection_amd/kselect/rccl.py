@@ -84,6 +84,7 @@ class RcclComm:
             raise RuntimeError("RCCL unique id: bad broadcast")
         ctypes.memmove(ctypes.addressof(uid), obj[0], 128)
         self._comm = ctypes.c_void_p()
+        self._eps = None
         with torch.cuda.device(device):
             _check(lib.ncclCommInitRank(ctypes.byref(self._comm), self.world, uid, self.rank), "ncclCommInitRank")
 
@@ -99,6 +100,14 @@ class RcclComm:
         """out[r * inp.numel() ..] = rank r's inp (int32 / uint32 words)."""
         _check(_lib.ncclAllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), _NCCL_UINT32, self._comm,
                                   self._s()), "ncclAllGather")
+
+    def entry_points(self):
+        """(communicator, ncclAllReduce, ncclAllGather) addresses of the RCCL copy
+        this communicator came from (kth_dist_select_rccl calls through them)."""
+        if self._eps is None or self._eps[0] != self._comm.value:
+            self._eps = (self._comm.value, ctypes.cast(_lib.ncclAllReduce, ctypes.c_void_p).value,
+                         ctypes.cast(_lib.ncclAllGather, ctypes.c_void_p).value)
+        return self._eps
 
     def close(self):
         if self._comm:

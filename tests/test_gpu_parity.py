@@ -537,11 +537,16 @@ def test_topk_rows_errors(gpu):
 
 
 # ----------------------------------------------------- sharded, one rank
-def test_dist_world1_nccl(gpu):
-    """The sharded protocol (kth_dist_* + RCCL collectives) with one rank."""
+@pytest.mark.parametrize("path", ["c", "py"])
+def test_dist_world1_nccl(gpu, monkeypatch, path):
+    """The sharded protocol (kth_dist_* + RCCL collectives) with one rank: over
+    RCCL in one library call (kth_dist_select_rccl, the default) or as the
+    scripted steps (KTH_DIST_PY=1), and over torch.distributed's collectives."""
     import torch
     import torch.distributed as dist
     from kselect.dist import DistSelector, HipBackend
+    if path == "py":
+        monkeypatch.setenv("KTH_DIST_PY", "1")
     # one rank over an in-process HashStore: no TCP port to race for
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0),
                             store=dist.HashStore())
@@ -558,6 +563,7 @@ def test_dist_world1_nccl(gpu):
                 for k in (1, n // 2, n):
                     got = int(ds.select(keys, n, n, k).item())
                     assert got == srt[k - 1], (fam, k, type(ds.comm).__name__, b.sel.stats())
+                    assert ds.error() == 0
             ds.close()
     finally:
         dist.destroy_process_group()

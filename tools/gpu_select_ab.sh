@@ -17,6 +17,6 @@ for v in base $VARIANTS; do
   f=${v//[:=]/_}
   python3 -c "
 import json
-v = [json.loads(l) for l in open('$O/$f.jsonl')]
+v = [json.loads(l) for l in open('$O/$f.jsonl') if l.startswith('{')]
 print('$v', ' '.join('%.1f' % d['value'] for d in v), 'Gkeys/s; ms', ' '.join('%.4f' % d['ms_per_step'] for d in v), 'verified', all(d['verified'] for d in v))"
 done
