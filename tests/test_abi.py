@@ -214,6 +214,26 @@ def test_protocol_constants_exported(lib):
     assert idx.size == (1 << 18) + 64 and idx[1024] == (1 << 24) // 257 and idx[-1] == 256 * ((1 << 24) // 257) + 63
 
 
+def test_dist_one_call_and_test_hook_argument_checks(lib):
+    """kth_dist_select_rccl and kth_ctx_test_hook refuse a missing ctx / null
+    pointers / bad values with KTH_EINVAL before touching a device."""
+    import kselect
+    one = ctypes.c_void_p(1)
+    args = [one, one, one, 2, one, 1 << 20, 1 << 21, 5, one, one, one, 1024, one, 1]
+    assert lib.kth_dist_select_rccl(None, *args) == kselect.KTH_EINVAL
+    for i in (0, 1, 2, 4, 8, 9, 10, 12):  # each pointer NULL in turn
+        bad = list(args)
+        bad[i] = None
+        assert lib.kth_dist_select_rccl(one, *bad) == kselect.KTH_EINVAL, i
+    bad = list(args)
+    bad[11] = 32  # a per-rank sample under 64 keys
+    assert lib.kth_dist_select_rccl(one, *bad) == kselect.KTH_EINVAL
+    bad = list(args)
+    bad[3] = 0  # world
+    assert lib.kth_dist_select_rccl(one, *bad) == kselect.KTH_EINVAL
+    assert lib.kth_ctx_test_hook(None, kselect.KTH_HOOK_FAULT_BARRIER, 1) == kselect.KTH_EINVAL
+
+
 @pytest.mark.parametrize("first", ["kselect", "torch"])
 def test_one_hip_runtime_whatever_the_import_order(first):
     """libkth.so and torch share ONE HIP runtime in a process, whichever is

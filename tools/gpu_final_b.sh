@@ -29,6 +29,9 @@ for k in 1048576 67108864 134217728 536870912; do
   pmc2 topk_$k -- --workload topk --k $k --steps 3 --warmup 1 --no-cpu-baseline
   python3 tools/pmc_topk.py $(csv topk_$k FETCH_SIZE) $(csv topk_$k WRITE_SIZE) 30 uniform_half $k $O/pmc_traffic_topk_k$k.json
 done
+echo "== request sizes of the staged pass (k_main<5>, dword loads since round 6): TCC_EA0_RDREQ vs its 128-B part"
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum -d $O/rdreq_tk -o run --output-format csv -- python3 bench.py --workload topk --k 67108864 --steps 3 --warmup 1 --no-cpu-baseline > $O/rdreq_tk.log 2>&1 || { echo rdreq rc=$?; tail -20 $O/rdreq_tk.log; exit 1; }
+python3 tools/sq_mix.py $O/rdreq_tk "k_main<5>" 64 "k_main<5> k=2^26 read requests per launch (x 64 keys: raw counts)"
 echo "== 2^33 lines"
 timeout -k 10 300 python -u bench.py --log2n 33 --steps 10 --warmup 3 --no-cpu-baseline > $O/b33.log 2>&1 || { echo b33 rc=$?; tail -20 $O/b33.log; exit 1; }
 tail -1 $O/b33.log | cut -c1-300
