@@ -12,9 +12,10 @@ collectives TODO-kth-problem-cgm.c:53-61, :103, :135-190.
 * bench.py --gpus 2 with KTH_SHARE_GPU=1 at 2^24 keys per rank: launcher, file
   rendezvous, the timed protocol, the device-side rank certificate; its line
   says it is not a scaling point.
-* The reference's golden fixtures split 2 ways by its block partition
+* The reference's golden fixtures split 2 and 3 ways by its block partition
   (TODO-kth-problem-cgm.c:81-100): every answer equals the true order
-  statistic and every terminating `mpirun -n 2` CGM-ref answer, on both ranks.
+  statistic and every terminating `mpirun -n 2` / `-n 3` CGM-ref answer, on
+  every rank.
 """
 import json
 import os
@@ -83,26 +84,31 @@ def _run_workers(world, timeout=240):
         os.rmdir(rdv_dir)
 
 
-def test_shared_gpu_golden_split_p2(golden):
-    """Two rank processes on GPU 0: the golden fixtures by the reference's
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_gpu_golden_split(golden, world):
+    """world rank processes on GPU 0: the golden fixtures by the reference's
     block partition (shards under 64 keys take the gather-to-every-rank path),
-    then 2^24 + 5 keys of three families, k in {1, n/3, n/2, n}."""
-    res = _run_workers(2)
-    assert sorted(res) == [0, 1]
+    every answer equal on every rank, to the true value and to every
+    terminating `mpirun -n world` CGM-ref run; then 2^24 + 5 keys of three
+    families (uneven shards at world 3), k in {1, n/3, n/2, n}."""
+    res = _run_workers(world)
+    assert sorted(res) == list(range(world))
     cases = golden["cases"]
-    g0, g1 = res[0]["golden"], res[1]["golden"]
-    assert len(g0) == len(g1) == len(cases)
+    gs = [res[r]["golden"] for r in range(world)]
+    assert all(len(g) == len(cases) for g in gs)
     checked_cgm = 0
-    for (i, a0, e0), (j, a1, e1) in zip(g0, g1):
+    for rows in zip(*gs):
+        i = rows[0][0]
         c = cases[i]
-        assert i == j and e0 == e1 == 0, (c, e0, e1)
-        assert a0 == a1 == c["true"], (c, a0, a1)
-        v = c["cgm_ref"].get("2")
+        assert all(r[0] == i and r[2] == 0 for r in rows), (c, rows)
+        assert {r[1] for r in rows} == {c["true"]}, (c, rows)
+        v = c["cgm_ref"].get(str(world))
         if v is not None and v != "livelock":
-            assert a0 == v, (c, a0)
+            assert rows[0][1] == v, (c, rows[0][1])
             checked_cgm += 1
     assert checked_cgm > 100  # (57 of the 190 P = 2 reference runs livelock)
-    s0, s1 = res[0]["synthetic"], res[1]["synthetic"]
-    assert len(s0) == len(s1) == 12
-    for (fam, n, k, a0, e0, want), (_, _, _, a1, e1, _) in zip(s0, s1):
-        assert e0 == e1 == 0 and a0 == a1 == want, (fam, n, k, a0, a1, want)
+    ss = [res[r]["synthetic"] for r in range(world)]
+    assert all(len(x) == 12 for x in ss)
+    for rows in zip(*ss):
+        fam, n, k, _, _, want = rows[0]
+        assert all(r[4] == 0 and r[3] == want for r in rows), (fam, n, k, rows)
