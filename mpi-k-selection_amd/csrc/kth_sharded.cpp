@@ -113,6 +113,7 @@ struct Dev {
     int32_t *out = nullptr;
     int32_t *staging = nullptr;  // device 0: the union, small / unbalanced inputs
     int64_t staging_cap = 0;
+    int32_t *d_status = nullptr;  // the handle's host status words, as this device addresses them
 };
 
 int grow(int device, void **p, int64_t *cap, int64_t bytes) {
@@ -249,6 +250,14 @@ int kth_sharded_create(const int *devices, int ngpu, kth_sharded **out) {
                           hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void **>(&h->d_status), h->h_status, 0) != hipSuccess)
             rc = KTH_ENOMEM;
+        // each device's own mapping of the (portable) words: no reliance on
+        // one address serving every device
+        for (size_t i = 0; rc == KTH_OK && i < h->d.size(); ++i) {
+            Dev &x = h->d[i];
+            if (hipSetDevice(x.device) != hipSuccess ||
+                hipHostGetDevicePointer(reinterpret_cast<void **>(&x.d_status), h->h_status, 0) != hipSuccess)
+                rc = KTH_EHIP;
+        }
     }
     if (rc == KTH_OK && !local) {
         if (rccl().CommInitAll(comms.data(), ngpu, devices) != ncclSuccess)
@@ -416,7 +425,7 @@ int kth_sharded_select_i32(kth_sharded *h, const int32_t *const *shards, const i
     } else {
         for (int i = 0; i < P; ++i) {
             Dev &x = h->d[(size_t)i];
-            TRY(kth_internal_status_gather(&x.ctx, 1, h->d_status + 2 * i, x.stream));
+            TRY(kth_internal_status_gather(&x.ctx, 1, x.d_status + 2 * i, x.stream));
         }
     }
     h->enqueue_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
