@@ -1095,7 +1095,12 @@ int kth_topk_i32(kth_ctx *c, const int32_t *d_keys, int64_t n, int64_t k, int la
         const u64 G = (u64)c->main_grid[tf];
         nwin = (uint32_t)(((nfull + G - 1) / G + kth::TK5_WIN_TILES - 1) / kth::TK5_WIN_TILES);
         KTH_TRY(grow(reinterpret_cast<void **>(&c->tk_wstart), &c->tk_wstart_cap, nwaves * std::max(nwin, 1u) * 4));
-        c->tk_seg = kth::TkSeg{c->tk_segv, c->tk_segp, (uint32_t)seg_cap, tflags + 3, c->tk_wstart, nwin};
+        // dense staging (k >= n / 32) stores the segments non-temporally: k_main<5> at k = 2^26 964-976
+        // against 980-984 us, whole calls -0.5 to -2 %; at k = 2^24 k_main<5> gains ~6 us but
+        // k_tk5_count, which then reads the entries from HBM, loses ~8; at 2^20 +0.8 %
+        // (profiles/r6_topk_seg_store_ab.txt)
+        const uint32_t nt = (u64)k * 32 >= (u64)n ? 1u : 0u;
+        c->tk_seg = kth::TkSeg{c->tk_segv, c->tk_segp, (uint32_t)seg_cap, tflags + 3, c->tk_wstart, nwin, nt};
     }
     // the k-th smallest (largest: the (n-k+1)-th smallest) -> d_status[0], on the device
     int64_t rank = largest ? n - k + 1 : k;

@@ -858,6 +858,7 @@ struct TkSeg {
     uint32_t *ovf;     // set to 1 when any segment overflows
     uint32_t *wstart;  // nwaves * nwin: entries a wave staged before each window of TK5_WIN_TILES tiles
     uint32_t nwin;     // windows per wave
+    uint32_t nt;       // 1: segment stores with the non-temporal hint (dense staging, k >= n / 32)
 };
 constexpr int TK5_WIN_TILES = 8;  // a window of the staged top-k kernels: 8 tiles = 64 wave-rows a wave
 
@@ -914,8 +915,15 @@ struct OrdStager {
                 const uint32_t g = (uint32_t)((h * FH + j) * WAVE + lane), e = 4 * g;
 #ifndef KTH_DIAG_TK5_NOSEGSTORE  // diagnostic builds only (wrong top-k results): cost of the segment stores
                 if (e + 4 <= n4 && e + 4 <= room) {
-                    *reinterpret_cast<uint4 *>(seg.vals + base + e) = kv[j];
-                    *reinterpret_cast<uint32_t *>(seg.pos + base + e) = pv[j];
+                    if (seg.nt) {  // wave-uniform
+                        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                        const v4u kvv = {kv[j].x, kv[j].y, kv[j].z, kv[j].w};
+                        __builtin_nontemporal_store(kvv, reinterpret_cast<v4u *>(seg.vals + base + e));
+                        __builtin_nontemporal_store(pv[j], reinterpret_cast<uint32_t *>(seg.pos + base + e));
+                    } else {
+                        *reinterpret_cast<uint4 *>(seg.vals + base + e) = kv[j];
+                        *reinterpret_cast<uint32_t *>(seg.pos + base + e) = pv[j];
+                    }
                 } else if (last && e < nw) {  // the last 1-3 entries (unaligned tail)
                     const uint32_t kq[4] = {kv[j].x, kv[j].y, kv[j].z, kv[j].w};
 #pragma unroll
