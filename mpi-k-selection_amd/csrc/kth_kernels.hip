@@ -35,6 +35,15 @@ constexpr int MAIN_SUB = MAIN_UNROLL < 8 ? MAIN_UNROLL : 8;  // loads per scanne
 #define KTH_WREG 2048
 #endif
 constexpr int WREG = KTH_WREG;        // per-wave candidate staging region (words of LDS)
+#ifndef KTH_WREG5
+#define KTH_WREG5 2496
+#endif
+// k_main<5/6>'s per-wave region (the ordered staging of the top-k): as large as
+// 4 workgroups a CU allow (40432 of 40960 B of LDS each).  Every flush of a
+// region costs the streaming wave the wait for its stores, so fewer, larger
+// flushes: 1984 entries instead of 1600, k_main<5> at k = 2^26 968-975 ->
+// 947 us, whole calls -1.5 % (2^24 -1 %; profiles/r6_topk_seg_store_ab.txt)
+constexpr int WREG5 = KTH_WREG5;
 constexpr int LEVEL_UNROLL = 8;       // 16-B loads in flight per thread in k_level
 constexpr int DENSE_BLK = 1024;       // workgroup size of the dense-histogram levels
 #ifndef KTH_SAMPLE_CK
@@ -863,7 +872,7 @@ struct TkSeg {
 constexpr int TK5_WIN_TILES = 8;  // a window of the staged top-k kernels: 8 tiles = 64 wave-rows a wave
 
 struct OrdStager {
-    static constexpr uint32_t CAP = ((uint32_t)WREG * 4 / 5) & ~63u;  // keys; CAP position bytes follow
+    static constexpr uint32_t CAP = ((uint32_t)WREG5 * 4 / 5) & ~63u;  // keys; CAP position bytes follow
     uint32_t *reg;
     uint32_t wfill;      // wave-uniform
     uint32_t seg_fill;   // wave-uniform: entries already in the segment
@@ -1033,7 +1042,7 @@ struct OrdStager {
         return total;
     }
 };
-static_assert(OrdStager::CAP + OrdStager::CAP / 4 <= (uint32_t)WREG && OrdStager::CAP >= 4 * WAVE,
+static_assert(OrdStager::CAP + OrdStager::CAP / 4 <= (uint32_t)WREG5 && OrdStager::CAP >= 4 * WAVE && WREG <= WREG5,
               "OrdStager region: keys + position bytes in one wave's region, >= one wave-row");
 
 // Count and stage K keys of this lane (key j valid iff bit j of `valid`).  The
@@ -1141,7 +1150,7 @@ __global__ __launch_bounds__(BLK) void k_main(StepArgs a, uint32_t *__restrict__
     static_assert(U % S == 0, "MAIN_UNROLL is a multiple of MAIN_SUB");
     __shared__ SelState ss;
     __shared__ u64 scratch[2 * (BLK / WAVE) + 8];
-    __shared__ __attribute__((aligned(16))) uint32_t region[BLK / WAVE][WREG];
+    __shared__ __attribute__((aligned(16))) uint32_t region[BLK / WAVE][TF >= 5 ? WREG5 : WREG];
     __shared__ u64 red[6][BLK / WAVE];
     __shared__ uint32_t rowx[BLK / WAVE][4];  // k_main<3/4>: a wave's row sums in transit
     KTH_STAMP(a, 0);
