@@ -597,8 +597,18 @@ __global__ __launch_bounds__(TK_BLOCK) void k_tk5_count(const int32_t *__restric
 // directly.  The next window's row records are loaded while this one is
 // placed and copied (the loop is a chain of dependent loads and barriers).
 // output entries a workgroup stages: 4096 (24 KiB of LDS) for k <= n / 32,
-// 8192 (48 KiB) above (a window of 64 Ki keys then holds ~k / n * 64 Ki outputs)
-constexpr int TK5_STAGE_SMALL = 4096, TK5_STAGE_LARGE = 8192;
+// 6144 (36 KiB) above (a window of 64 Ki keys then holds ~k / n * 64 Ki outputs)
+// (round 6: 6144 instead of 8192 for the large stage, 36.9 instead of 49.3 KiB
+// of LDS: 4 workgroups a CU instead of 3; k_tk5_write at k = 2^26 404 -> 372
+// us, whole call -1.8 %; a window of 64 Ki keys holds ~k / n * 64 Ki <= 4096
+// outputs on the staged path, profiles/r6_topk_seg_store_ab.txt)
+#ifndef KTH_TK5_STAGE_LARGE
+#define KTH_TK5_STAGE_LARGE 6144
+#endif
+#ifndef KTH_TK5_STAGE_SMALL
+#define KTH_TK5_STAGE_SMALL 4096
+#endif
+constexpr int TK5_STAGE_SMALL = KTH_TK5_STAGE_SMALL, TK5_STAGE_LARGE = KTH_TK5_STAGE_LARGE;
 struct Tk5Rec {                  // one lane's row records of a window
     uint32_t c, tc;              // the wave-row's entries; the row's count word
     u64 off, b0, b1;             // toff[r], bbase[2 blk], bbase[2 blk + 1]
